@@ -1,0 +1,245 @@
+/*
+ * imenv.h — C ABI of the MI355X-native vectorised inventory-management env.
+ *
+ * This is the drop-in boundary for the hot path named in BASELINE.json
+ * (north_star): the reset()/step() dynamics of the reference's four env classes
+ *
+ *   environments/IM_env.py        InvManagement.reset/step          (:164-229, :287-360)
+ *   environments/MAIM_env.py      MultiAgentInvManagement.reset/step (:176-240, :330-411)
+ *   environments/IM_div_env.py    InvManagementDiv.reset/step        (:201-302, :361-549)
+ *   environments/MAIM_div_env.py  MultiAgentInvManagementDiv.reset/step (:240-341, :441-630)
+ *
+ * batched over n_envs independent envs that advance in lockstep. The reference
+ * is pure Python, so there is no FFI to mirror line by line; each entry point
+ * below names the reference method it replaces. Host-side adaptors that
+ * re-expose the reference's gym/RLlib surface over this ABI live in
+ * marl-for-im_amd/imenv (ctypes), see INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain C types only. Every buffer argument is a DEVICE pointer owned by the
+ *    caller unless stated otherwise; the handle owns its state buffers.
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream). All
+ *    calls are stream-ordered and asynchronous unless stated otherwise.
+ *  - Return value: IMENV_OK (0) or a negative IMENV_E_* code; the message is
+ *    available from imenv_last_error() (thread-local). No exceptions cross the ABI.
+ *  - One handle per (process, GPU); not thread-safe per handle.
+ *
+ * Node indexing is the reference's own: serial envs use stage 0 = retailer,
+ * stage N-1 = factory; tree envs use node 0 = factory (root), leaves = retailers.
+ */
+#ifndef IMENV_H
+#define IMENV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IMENV_ABI_VERSION 1
+
+#define IMENV_MAX_NODES 16
+#define IMENV_MAX_CHILDREN 8
+#define IMENV_MAX_FEATURES 64
+#define IMENV_MAX_HIST 8
+#define IMENV_MAX_DELAY 64
+#define IMENV_MAX_PERIODS 100000
+
+/* status codes */
+#define IMENV_OK 0
+#define IMENV_E_INVALID -1      /* bad argument / spec (reference: Exception / assert at __init__) */
+#define IMENV_E_UNSUPPORTED -2  /* valid in the reference but not supported by this build */
+#define IMENV_E_HIP -3          /* HIP runtime error */
+#define IMENV_E_DONE -4         /* step() past num_periods (reference: IndexError) */
+#define IMENV_E_NOT_RESET -5    /* step() before the first reset() */
+#define IMENV_E_SPLIT_LOOP -6   /* an env tripped the divergent split's "Infinite Loop" guard */
+
+/* env class whose semantics the spec encodes (documentation + validation only;
+ * every behavioural difference is spelled out in the spec fields) */
+#define IMENV_KIND_IM 0
+#define IMENV_KIND_MAIM 1
+#define IMENV_KIND_IM_DIV 2
+#define IMENV_KIND_MAIM_DIV 3
+
+/* order decode: IM / IM_div clip then round (IM_env.py:299-300);
+ * MAIM / MAIM_div round then clip (MAIM_env.py:343-347) */
+#define IMENV_DECODE_CLIP_ROUND 0
+#define IMENV_DECODE_ROUND_CLIP 1
+
+/* reward: single-agent np.sum(profit) in NumPy's summation order (IM_env.py:372);
+ * multi-agent shared (0 + p0 + ... + pN-1) / N (MAIM_env.py:418-434);
+ * multi-agent independent profit per agent (MAIM_env.py:428-429) */
+#define IMENV_REWARD_SUM 0
+#define IMENV_REWARD_SHARED_MEAN 1
+#define IMENV_REWARD_INDEPENDENT 2
+
+/* observation feature groups (IM_env.py:231-285 etc.) */
+#define IMENV_G_INV 0
+#define IMENV_G_BACKLOG 1
+#define IMENV_G_ORDER_U 2
+#define IMENV_G_DEMAND_HIST 3   /* index j: demand at period t-1-j (0 when j >= t) */
+#define IMENV_G_ORDER_HIST 4    /* index j: order at period t-1-j (0 when j >= t) */
+#define IMENV_G_TRANSIT 5       /* index k: in-transit amount arriving at t+k ("time_dependent_state") */
+#define IMENV_G_NODE_ID 6       /* share_network agent id (MAIM_div_env.py:434-435) */
+#define IMENV_G_ZERO 7          /* always 0 (MAIM unstandardised history slots) */
+#define IMENV_NUM_GROUPS 8
+
+/* how a group's raw value v becomes an observation */
+#define IMENV_OBS_ZERO 0
+#define IMENV_OBS_RAW 1           /* v */
+#define IMENV_OBS_SCALED 2        /* a + (v * (b - a)) / den   (rescale, IM_env.py:435-444) */
+#define IMENV_OBS_CLAMP_SCALED 3  /* a + (min(v, clip) * (b - a)) / den  (MAIM_div_env.py:405-411) */
+
+/* what reset() draws when the caller passes no demand (spec.demand_dist) */
+#define IMENV_DEMAND_CUSTOM 1    /* the caller must pass a table (the reference's "custom") */
+#define IMENV_DEMAND_POISSON 2   /* in-kernel Philox4x32-10 + inversion, Poisson(mu) */
+#define IMENV_DEMAND_UNIFORM 3   /* in-kernel Philox4x32-10, randint[low, high) */
+
+/* imenv_reset demand_layout */
+#define IMENV_LAYOUT_DRAW 0      /* demand == NULL: draw per spec.demand_dist (+ noisy demand) */
+#define IMENV_LAYOUT_PER_ENV 1   /* device int32 [T][R][n]: reset(customer_demand=...) per env */
+#define IMENV_LAYOUT_BROADCAST 2 /* device int32 [T][R]: one custom table for every env (+ noisy demand) */
+
+/* dtypes */
+#define IMENV_F32 0
+#define IMENV_F64 1
+
+typedef struct ImEnvSpec {
+  int32_t abi_version;          /* = IMENV_ABI_VERSION */
+  int32_t kind;                 /* IMENV_KIND_* */
+  int32_t num_nodes;            /* N <= IMENV_MAX_NODES */
+  int32_t num_periods;          /* T */
+
+  /* topology: parent[i] = upstream node (-1 for the factory); children in the
+   * reference's iteration order (connections[p] list order, IM_div_env.py:415) */
+  int32_t parent[IMENV_MAX_NODES];
+  int32_t num_children[IMENV_MAX_NODES];
+  int32_t children[IMENV_MAX_NODES][IMENV_MAX_CHILDREN];
+  /* demand_parent[c]: node whose demand includes c's order (-1: none). Serial:
+   * c+1; tree: parent if c > parent (IM_div_env.py:383-387 scans j >= i) */
+  int32_t demand_parent[IMENV_MAX_NODES];
+  /* retailer_slot[i]: row of the customer-demand table for retailer i, else -1 */
+  int32_t retailer_slot[IMENV_MAX_NODES];
+  int32_t num_retailers;
+
+  int32_t delay[IMENV_MAX_NODES];       /* lead time, >= 1 in this build */
+  /* integral capacities (the reference keeps them as float64) */
+  int32_t init_inv[IMENV_MAX_NODES];
+  int32_t inv_max[IMENV_MAX_NODES];
+  int32_t order_max[IMENV_MAX_NODES];
+  int32_t backlog_cap[IMENV_MAX_NODES]; /* -1 = uncapped */
+  /* divergent split guard limits (IM_div_env.py:424,449,483,497): rounds > limit trips */
+  int32_t split_limit[IMENV_MAX_NODES][4];
+
+  double sell_price[IMENV_MAX_NODES];   /* serial price[i]; tree stage+2 */
+  double buy_price[IMENV_MAX_NODES];    /* serial price[i+1]; tree stage+1 */
+  double stock_cost[IMENV_MAX_NODES];
+  double backlog_cost[IMENV_MAX_NODES];
+  double inv_target[IMENV_MAX_NODES];
+
+  /* action decode */
+  int32_t standardise_actions;  /* 1: order = rev_scale(x), else x */
+  int32_t decode_mode;          /* IMENV_DECODE_* */
+  double a, b;                  /* scaling interval (rescale / rev_scale) */
+
+  int32_t reward_mode;          /* IMENV_REWARD_* */
+
+  /* observation: num_features entries of (group, index); per group a mode and
+   * a per-node denominator (and clip for CLAMP_SCALED) */
+  int32_t num_features;
+  int32_t feat_group[IMENV_MAX_FEATURES];
+  int32_t feat_index[IMENV_MAX_FEATURES];
+  int32_t group_mode[IMENV_NUM_GROUPS];
+  double group_den[IMENV_NUM_GROUPS][IMENV_MAX_NODES];
+  double group_clip[IMENV_NUM_GROUPS][IMENV_MAX_NODES];
+  int32_t prev_length;          /* L: history depth kept for DEMAND/ORDER_HIST */
+
+  /* demand */
+  int32_t demand_dist;          /* IMENV_DEMAND_*: what reset() draws with IMENV_LAYOUT_DRAW */
+  double poisson_mu;
+  int32_t uniform_low, uniform_high;
+  int32_t noisy_demand;         /* div envs: double w.p. thr, then zero w.p. thr (IM_div_env.py:246-255) */
+  double noisy_demand_threshold;
+  int32_t noisy_delay;          /* initial latch (div envs read it from config, IM_div_env.py:50-51) */
+  double noisy_delay_threshold;
+  uint64_t seed;                /* Philox key */
+} ImEnvSpec;
+
+typedef struct ImEnv ImEnv;
+
+/* Optional per-step outputs (the reference's `info` dict, IM_env.py:345-350 and
+ * MAIM_env.py:399-409, plus the split state). Any pointer may be NULL.
+ * int32 [n][N] unless noted. */
+typedef struct ImEnvInfo {
+  int32_t* order;        /* 'actual order' (order_r[t]) */
+  int32_t* demand;       /* demand[t] */
+  int32_t* acquisition;  /* acquisition[t] */
+  int32_t* ship;         /* ship[t] */
+  double* profit;        /* double [n][N] */
+  int32_t* ship_to;      /* amount shipped INTO node c at t (ship_to_list[t][parent][c]) */
+  int32_t* backlog_to;   /* backlog_to[parent][c] after the step (0 unless parent splits) */
+} ImEnvInfo;
+
+/* Replaces the constructors: InvManagement.__init__ (IM_env.py:7-162),
+ * MultiAgentInvManagement.__init__ (MAIM_env.py:8-173), InvManagementDiv.__init__
+ * (IM_div_env.py:9-199), MultiAgentInvManagementDiv.__init__ (MAIM_div_env.py:9-237).
+ * The caller derives the spec from the reference config dict (imenv/spec.py).
+ * env_offset = global id of this handle's first env (RNG key; sharding). */
+int imenv_create(const ImEnvSpec* spec, int64_t n_envs, int64_t env_offset, int device, ImEnv** out);
+
+/* Replaces reset(customer_demand=None, noisy_delay=False, noisy_delay_threshold=0)
+ * (IM_env.py:164-229 and siblings). Writes the period-0 observation to obs
+ * ([n][N][F], obs_dtype). demand / demand_layout: IMENV_LAYOUT_* above (the
+ * table is copied; the caller may free it after the call is stream-ordered).
+ * Noisy demand (div envs, IM_div_env.py:246-255) applies to drawn and broadcast
+ * demand only, as in the reference (not to demand passed per env).
+ * noisy_delay != 0 latches noisy delay with the given threshold, as the reference
+ * does (IM_env.py:180-182). delay_uniforms: optional device double [T][N][n] —
+ * host-fed uniforms for the noisy-delay draw (u <= threshold; bit-exact parity
+ * path); NULL = in-kernel Philox. episode: Philox counter word for this
+ * episode; pass -1 to auto-increment (first reset -> 0). */
+int imenv_reset(ImEnv* env, const int32_t* demand, int demand_layout, int noisy_delay,
+                double noisy_delay_threshold, const double* delay_uniforms, int64_t episode, void* obs,
+                int obs_dtype, void* stream);
+
+/* Replaces step(action) / step(action_dict) (IM_env.py:287-360 and siblings).
+ * actions: device [n][N] (action_dtype IMENV_F32 / IMENV_F64; f32 is promoted to
+ * f64 before decoding, as the reference's ndarray path does). obs: [n][N][F]
+ * (obs_dtype). reward: double [n] (SUM / SHARED_MEAN) or [n][N] (INDEPENDENT).
+ * info: optional. done_out (HOST int*, may be NULL) receives period >= T. */
+int imenv_step(ImEnv* env, const void* actions, int action_dtype, void* obs, int obs_dtype,
+               double* reward, const ImEnvInfo* info, int32_t* done_out, void* stream);
+
+/* State the reference's callers read directly (base_restock_policy.py:12:
+ * env.inv/order_u/backlog[env.period]). Copies int32 [N][n] SoA into the given
+ * device buffers (any may be NULL); *period (HOST) receives the current period. */
+int imenv_get_state(ImEnv* env, int32_t* inv, int32_t* backlog, int32_t* order_u, int32_t* period,
+                    void* stream);
+
+/* Divergent-split guard trips ("Infinite Loop 1-4", MAIM_div_env.py:505-575):
+ * per-env flags (device uint32 [n], may be NULL) and, synchronously, the OR of
+ * all flags since the last reset into *any_out (HOST). */
+int imenv_get_errors(ImEnv* env, uint32_t* flags, uint32_t* any_out, void* stream);
+
+/* Shapes: number of nodes, observation features per node, customer-demand rows. */
+int imenv_dims(const ImEnv* env, int32_t* num_nodes, int32_t* num_features, int32_t* num_retailers,
+               int32_t* num_periods);
+
+/* Inversion table used for in-kernel Poisson draws (uint32 thresholds, HOST
+ * buffer of capacity `cap`); *len_out receives the table length. */
+int imenv_poisson_table(const ImEnv* env, uint32_t* out, int32_t cap, int32_t* len_out);
+
+void imenv_destroy(ImEnv* env);
+
+const char* imenv_last_error(void);
+
+int imenv_abi_version(void);
+
+/* sizeof(ImEnvSpec) as compiled into the library (binding layout check). */
+int64_t imenv_spec_size(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* IMENV_H */

@@ -1,0 +1,24 @@
+"""imenv — MI355X-native vectorised inventory-management environment.
+
+Host side of the hot path: a HIP kernel library (csrc/imenv_kernels.hip, C ABI in
+include/imenv.h) driven from Python. Public surface:
+
+  build_spec(kind, config)      reference config dict -> HostSpec (spec.py)
+  VectorInvEnv(kind, config, n) batched envs on one GPU (vector_env.py)
+  InvManagement, MultiAgentInvManagement, InvManagementDiv,
+  MultiAgentInvManagementDiv    drop-in single-env adaptors (envs.py)
+
+torch is imported lazily so that the spec builder works without a GPU stack.
+"""
+from .spec import HostSpec, SpecError, build_spec  # noqa: F401
+from ._native import ImEnvNativeError  # noqa: F401
+
+
+def __getattr__(name):
+    if name == "VectorInvEnv":
+        from .vector_env import VectorInvEnv
+        return VectorInvEnv
+    if name in ("InvManagement", "MultiAgentInvManagement", "InvManagementDiv", "MultiAgentInvManagementDiv"):
+        from . import envs
+        return getattr(envs, name)
+    raise AttributeError(name)

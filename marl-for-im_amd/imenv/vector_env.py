@@ -1,0 +1,192 @@
+"""VectorInvEnv — a batch of n independent inventory envs resident in HBM.
+
+Python host over the C ABI (include/imenv.h). All buffers are torch tensors on
+the HIP device; every call is enqueued on the current torch stream of that
+device, so it composes with a torch policy without synchronisation. The envs
+advance in lockstep (all share the period t, as every reference env has a
+fixed horizon and no auto-reset).
+
+    env = VectorInvEnv("MAIM", env_config, n_envs=1 << 20)
+    obs = env.reset()                      # [n, N, F] float32, period 0
+    obs, reward, done, info = env.step(actions)   # actions [n, N] in [a, b]
+
+This replaces, batched, the reference's reset()/step() of the four env classes
+(environments/IM_env.py:164-360, MAIM_env.py:176-411, IM_div_env.py:201-549,
+MAIM_div_env.py:240-630). There is no CPU fallback: construction fails loudly
+without a HIP device or without libimenv.so.
+"""
+import ctypes
+from ctypes import byref, c_int32, c_uint32, c_void_p
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .spec import HostSpec, build_spec
+
+
+class VectorInvEnv:
+    def __init__(self, kind_or_spec, config=None, n_envs=1, device=None, env_offset=0,
+                 obs_dtype=torch.float32):
+        self.spec = kind_or_spec if isinstance(kind_or_spec, HostSpec) else build_spec(kind_or_spec, config or {})
+        if not torch.cuda.is_available():
+            raise nat.ImEnvNativeError("VectorInvEnv needs a HIP device; there is no CPU fallback")
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = device
+        self.n = int(n_envs)
+        self.env_offset = int(env_offset)
+        if obs_dtype not in (torch.float32, torch.float64):
+            raise ValueError("obs_dtype must be float32 or float64")
+        self.obs_dtype = obs_dtype
+        self.lib = nat.load()
+        self._c = self.spec.to_c()
+        h = c_void_p()
+        nat.check(self.lib.imenv_create(byref(self._c), self.n, self.env_offset, self.device.index, byref(h)),
+                  "imenv_create")
+        self._h = h
+        self.N = self.spec.num_nodes
+        self.F = self.spec.num_features
+        self.R = self.spec.num_retailers
+        self.T = self.spec.num_periods
+        self.period = 0
+        self.episode = -1
+        self._keep = []
+
+    # ------------------------------------------------------------------ helpers
+    def _stream(self):
+        return c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _obs_code(self, dtype):
+        return nat.F64 if dtype == torch.float64 else nat.F32
+
+    def reward_shape(self):
+        return (self.n, self.N) if self.spec.reward_mode == nat.REWARD_INDEPENDENT else (self.n,)
+
+    def _demand_tensor(self, customer_demand):
+        """-> (device int32 tensor, layout). Per-env [n,T] / [n,R,T] or broadcast [T] / [R,T]."""
+        cd = torch.as_tensor(np.asarray(customer_demand) if not torch.is_tensor(customer_demand)
+                             else customer_demand)
+        cd = cd.to(device=self.device, dtype=torch.int32)
+        T, R, n = self.T, self.R, self.n
+        if cd.shape[-1] < T:
+            raise ValueError("customer demand shorter than num_periods")
+        cd = cd[..., :T]
+        per_env = cd.dim() == (2 if self.spec.serial else 3)
+        if per_env:
+            # per env: serial [n, T] -> [T, 1, n]; tree [n, R, T] -> [T, R, n]
+            if cd.dim() == 2:
+                cd = cd[:, None, :]
+            if cd.shape[0] != n or cd.shape[1] != R:
+                raise ValueError("per-env demand must be [n, T] (serial) or [n, R, T] (tree)")
+            return cd.permute(2, 1, 0).contiguous(), nat.LAYOUT_PER_ENV
+        if cd.dim() == 1:
+            cd = cd[None, :]
+        if cd.dim() != 2 or cd.shape[0] != R:
+            raise ValueError("broadcast demand must be [T] (serial) or [R, T] (tree)")
+        return cd.t().contiguous(), nat.LAYOUT_BROADCAST
+
+    # ------------------------------------------------------------------ API
+    def reset(self, customer_demand=None, noisy_delay=False, noisy_delay_threshold=0.0,
+              delay_uniforms=None, episode=None, obs_out=None):
+        """reset(customer_demand=None, noisy_delay=False, noisy_delay_threshold=0) (IM_env.py:164).
+
+        customer_demand: per-env [n, T] (serial) / [n, R, T] (tree), or one table [T] / [R, T]
+        for every env; None draws from the spec's distribution in-kernel (Philox, keyed by
+        (seed, global env id, episode)). delay_uniforms: [n, T, N] float64 host-fed uniforms
+        for noisy delay (bit-exact parity), None = in-kernel draws.
+        """
+        keep = []
+        dptr, layout = None, nat.LAYOUT_DRAW
+        if customer_demand is not None:
+            d, layout = self._demand_tensor(customer_demand)
+            keep.append(d)
+            dptr = d.data_ptr()
+        elif self.spec.demand_dist == "custom":
+            d, layout = self._demand_tensor(self.spec.custom_demand)
+            keep.append(d)
+            dptr = d.data_ptr()
+        uptr = None
+        if delay_uniforms is not None:
+            u = torch.as_tensor(delay_uniforms).to(device=self.device, dtype=torch.float64)
+            if tuple(u.shape) != (self.n, self.T, self.N):
+                raise ValueError("delay_uniforms must be [n, T, N]")
+            u = u.permute(1, 2, 0).contiguous()
+            keep.append(u)
+            uptr = u.data_ptr()
+        obs = obs_out if obs_out is not None else torch.empty(
+            (self.n, self.N, self.F), dtype=self.obs_dtype, device=self.device)
+        ep = -1 if episode is None else int(episode)
+        nat.check(self.lib.imenv_reset(self._h, dptr, layout, int(bool(noisy_delay)), float(noisy_delay_threshold),
+                                       uptr, ep, obs.data_ptr(), self._obs_code(obs.dtype), self._stream()),
+                  "imenv_reset")
+        self._keep = keep          # the copies are stream-ordered; keep sources alive one call
+        self.period = 0
+        self.episode = self.episode + 1 if episode is None else int(episode)
+        return obs
+
+    def step(self, actions, obs_out=None, reward_out=None, info=False):
+        """step(action) (IM_env.py:287-360): actions [n, N] (or [n*N]) in the spec's action units."""
+        a = actions if torch.is_tensor(actions) else torch.as_tensor(np.asarray(actions))
+        if a.device != self.device or a.dtype not in (torch.float32, torch.float64):
+            a = a.to(device=self.device, dtype=torch.float64 if a.dtype == torch.float64 else torch.float32)
+        a = a.reshape(self.n, self.N).contiguous()
+        obs = obs_out if obs_out is not None else torch.empty(
+            (self.n, self.N, self.F), dtype=self.obs_dtype, device=self.device)
+        rew = reward_out if reward_out is not None else torch.empty(
+            self.reward_shape(), dtype=torch.float64, device=self.device)
+        inf = None
+        iptr = None
+        if info:
+            z = lambda dt: torch.empty((self.n, self.N), dtype=dt, device=self.device)
+            inf = dict(order=z(torch.int32), demand=z(torch.int32), acquisition=z(torch.int32),
+                       ship=z(torch.int32), profit=z(torch.float64), ship_to=z(torch.int32),
+                       backlog_to=z(torch.int32))
+            ci = nat.ImEnvInfo(*[inf[k].data_ptr() for k in ("order", "demand", "acquisition", "ship",
+                                                               "profit", "ship_to", "backlog_to")])
+            iptr = byref(ci)
+        done = c_int32(0)
+        nat.check(self.lib.imenv_step(self._h, a.data_ptr(), nat.F64 if a.dtype == torch.float64 else nat.F32,
+                                      obs.data_ptr(), self._obs_code(obs.dtype), rew.data_ptr(), iptr,
+                                      byref(done), self._stream()), "imenv_step")
+        self._keep = [a]
+        self.period += 1
+        return obs, rew, bool(done.value), inf
+
+    def state(self):
+        """inv / backlog / order_u at the current period as [n, N] int32 (base_restock_policy.py:12)."""
+        bufs = [torch.empty((self.N, self.n), dtype=torch.int32, device=self.device) for _ in range(3)]
+        p = c_int32()
+        nat.check(self.lib.imenv_get_state(self._h, bufs[0].data_ptr(), bufs[1].data_ptr(), bufs[2].data_ptr(),
+                                           byref(p), self._stream()), "imenv_get_state")
+        return dict(inv=bufs[0].t(), backlog=bufs[1].t(), order_u=bufs[2].t(), period=p.value)
+
+    def errors(self):
+        """Per-env split-guard flags ("Infinite Loop", MAIM_div_env.py:505-575) and their OR (syncs)."""
+        flags = torch.empty(self.n, dtype=torch.int32, device=self.device)
+        anyv = c_uint32()
+        nat.check(self.lib.imenv_get_errors(self._h, flags.data_ptr(), byref(anyv), self._stream()),
+                  "imenv_get_errors")
+        return flags, int(anyv.value)
+
+    def poisson_table(self):
+        ln = c_int32()
+        nat.check(self.lib.imenv_poisson_table(self._h, None, 0, byref(ln)), "imenv_poisson_table")
+        buf = (ctypes.c_uint32 * max(ln.value, 1))()
+        nat.check(self.lib.imenv_poisson_table(self._h, buf, ln.value, byref(ln)), "imenv_poisson_table")
+        return np.array(buf[:ln.value], dtype=np.uint64)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            torch.cuda.synchronize(self.device)
+            self.lib.imenv_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

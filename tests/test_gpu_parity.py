@@ -1,0 +1,210 @@
+"""HIP kernel parity: GPU step()/reset() vs the reference's golden vectors and the oracle.
+
+All comparisons are exact: integer state/intermediates bit-equal; float64 obs and
+rewards bit-equal to the reference's float64 (IEEE ops in the reference's order,
+no FMA contraction); float32 obs equal to float32(reference obs).
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import case_names, load_case
+from oracle import philox
+from oracle.im_oracle import OracleEnv
+
+pytestmark = pytest.mark.gpu
+
+CASES = case_names()
+DEV = "cuda:0"
+
+
+def _env(kind, cfg, n, **kw):
+    from imenv import VectorInvEnv
+    return VectorInvEnv(kind, cfg, n_envs=n, device=DEV, **kw)
+
+
+def run_gpu_case(meta, d, obs_dtype=torch.float64, action_dtype=torch.float64):
+    kind, cfg, E, T = meta["kind"], meta["config"], meta["E"], meta["T"]
+    env = _env(kind, cfg, E, obs_dtype=obs_dtype)
+    serial = kind in ("IM", "MAIM")
+    dem = d["customer_demand"]
+    noisy = meta["noisy"]
+    obs0 = env.reset(customer_demand=dem[:, 0, :] if serial else dem, noisy_delay=bool(noisy),
+                     noisy_delay_threshold=noisy, delay_uniforms=d["delay_uniforms"] if noisy else None)
+    out = {k: [] for k in ("order", "demand", "acquisition", "ship", "inv", "backlog", "order_u", "obs",
+                           "reward", "profit", "ship_to", "backlog_to")}
+    obs0 = obs0.cpu().numpy()
+    for t in range(T):
+        a = torch.as_tensor(d["actions"][:, t, :], dtype=action_dtype, device=DEV)
+        obs, rew, done, info = env.step(a, info=True)
+        st = env.state()
+        assert st["period"] == t + 1
+        assert done == (t == T - 1)
+        for k in ("order", "demand", "acquisition", "ship", "profit", "ship_to", "backlog_to"):
+            out[k].append(info[k].cpu().numpy())
+        for k in ("inv", "backlog", "order_u"):
+            out[k].append(st[k].cpu().numpy())
+        out["obs"].append(obs.cpu().numpy())
+        r = rew.cpu().numpy()
+        out["reward"].append(r if r.ndim == 2 else r[:, None])
+    flags, anyv = env.errors()
+    env.close()
+    return obs0, {k: np.stack(v, axis=1) for k, v in out.items()}, anyv
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_gpu_matches_reference_golden(name):
+    meta, d = load_case(name)
+    obs0, out, anyerr = run_gpu_case(meta, d)
+    assert anyerr == 0
+    np.testing.assert_array_equal(obs0, d["obs0"], err_msg="%s/obs0" % name)
+    keys = ["order", "demand", "acquisition", "ship", "inv", "backlog", "order_u", "profit", "obs"]
+    if meta["kind"] in ("IM_div", "MAIM_div"):
+        keys += ["ship_to", "backlog_to"]
+    for k in keys:
+        np.testing.assert_array_equal(out[k].astype(np.float64), d[k], err_msg="%s/%s" % (name, k))
+    ref_r = d["reward"]
+    if out["reward"].shape[-1] == 1:
+        ref_r = ref_r[..., :1]
+    np.testing.assert_array_equal(out["reward"], ref_r, err_msg="%s/reward" % name)
+
+
+@pytest.mark.parametrize("name", ["C1_IM4", "C2_MAIM4", "C3_IM8", "C4_MAIM_div1", "MAIM_div2_share",
+                                  "IM4_td_pd_pa_L2"])
+def test_gpu_float32_obs_is_rounded_reference(name):
+    meta, d = load_case(name)
+    obs0, out, _ = run_gpu_case(meta, d, obs_dtype=torch.float32)
+    np.testing.assert_array_equal(out["obs"], d["obs"].astype(np.float32))
+    np.testing.assert_array_equal(obs0, d["obs0"].astype(np.float32))
+
+
+C2 = dict(num_stages=4, num_periods=30, init_inv=np.ones(4) * 10, inv_target=np.zeros(4),
+          inv_max=np.ones(4) * 30, price=np.array([5, 4, 3, 2, 1]),
+          stock_cost=np.array([0.35, 0.3, 0.4, 0.2]), backlog_cost=np.array([0.5, 0.7, 0.6, 0.9]),
+          delay=np.array([1, 2, 3, 1]), demand_dist="poisson", mu=5, seed=52, independent=False)
+C3 = dict(num_stages=8, num_periods=30, init_inv=np.ones(8) * 10, inv_target=np.zeros(8),
+          inv_max=np.ones(8) * 30, price=np.array([9, 8, 7, 6, 5, 4, 3, 2, 1]),
+          stock_cost=np.array([0.35, 0.3, 0.4, 0.2, 0.35, 0.3, 0.4, 0.2]),
+          backlog_cost=np.array([0.5, 0.7, 0.6, 0.9, 0.5, 0.7, 0.6, 0.9]),
+          delay=np.array([1, 2, 3, 1, 4, 2, 3, 1]), demand_dist="poisson", mu=5, seed=52)
+C4 = dict(num_nodes=4, connections={0: [1], 1: [2, 3], 2: [], 3: []}, num_periods=30,
+          init_inv=np.ones(4) * 10, inv_target=np.zeros(4), inv_max=np.ones(4) * 30,
+          stock_cost=np.array([0.35, 0.3, 0.4, 0.4]), backlog_cost=np.array([0.5, 0.7, 0.6, 0.6]),
+          delay=np.array([1, 2, 1, 1]), demand_dist="poisson", mu=5, seed=52, time_dependency=True,
+          prev_demand=True, independent=False)
+
+
+@pytest.mark.parametrize("kind,cfg,n", [("MAIM", C2, 8192), ("IM", C3, 4096), ("MAIM_div", C4, 8192),
+                                         ("MAIM_div", dict(C4, noisy_demand=True, noisy_demand_threshold=0.3,
+                                                           demand_dist="uniform", lower_upper=(1, 9)), 4096)])
+def test_gpu_philox_rollout_matches_oracle(kind, cfg, n):
+    """In-kernel Philox demand + f32 actions over two episodes == oracle with the same counters."""
+    env = _env(kind, cfg, n, env_offset=1000)
+    ora = OracleEnv(kind, cfg, n_envs=n)
+    if cfg["demand_dist"] == "poisson":
+        np.testing.assert_array_equal(env.poisson_table(), philox.poisson_thresholds(cfg.get("mu", 5)))
+    rs = np.random.RandomState(7)
+    for ep in range(2):
+        env.reset()
+        ora.reset(rng=dict(seed=52, episode=ep, env_offset=1000, dist=cfg["demand_dist"], mu=cfg.get("mu", 5),
+                           lower_upper=cfg.get("lower_upper", (1, 5))))
+        for t in range(30):
+            a32 = rs.uniform(-1.1, 1.1, size=(n, env.N)).astype(np.float32)
+            o_g, r_g, _, info = env.step(torch.as_tensor(a32, device=DEV), info=True)
+            o_c, r_c, _, info_c = ora.step(a32.astype(np.float64))
+            np.testing.assert_array_equal(info["demand"].cpu().numpy(), info_c["demand"], err_msg="t=%d" % t)
+            st = env.state()
+            for k in ("inv", "backlog", "order_u"):
+                np.testing.assert_array_equal(st[k].cpu().numpy(), ora.state_arrays()[k])
+            np.testing.assert_array_equal(o_g.cpu().numpy(), o_c.astype(np.float32))
+            r_c = r_c if r_c.ndim == 2 else r_c
+            np.testing.assert_array_equal(r_g.cpu().numpy(), r_c)
+
+
+def test_gpu_philox_noisy_delay_matches_oracle():
+    cfg = dict(C2, time_dependency=True)
+    n = 4096
+    env = _env("MAIM", cfg, n)
+    ora = OracleEnv("MAIM", cfg, n_envs=n)
+    env.reset(noisy_delay=True, noisy_delay_threshold=0.3)
+    ora.reset(rng=dict(seed=52, episode=0, env_offset=0, mu=5), noisy_delay=True, noisy_delay_threshold=0.3)
+    rs = np.random.RandomState(3)
+    for t in range(30):
+        a = rs.uniform(-1, 1, size=(n, 4))
+        o_g, r_g, _, info = env.step(torch.as_tensor(a, device=DEV), info=True)
+        o_c, r_c, _, info_c = ora.step(a)
+        np.testing.assert_array_equal(info["acquisition"].cpu().numpy(), info_c["acquisition"])
+        np.testing.assert_array_equal(o_g.cpu().numpy(), o_c.astype(np.float32))
+        np.testing.assert_array_equal(r_g.cpu().numpy(), r_c)
+
+
+def test_gpu_sharding_invariance():
+    """Two handles at env_offset 0 and n/2 reproduce one handle of n envs (RNG keyed by global id)."""
+    n = 1 << 14
+    full = _env("MAIM", C2, n)
+    halves = [_env("MAIM", C2, n // 2, env_offset=r * (n // 2)) for r in range(2)]
+    full.reset()
+    for h in halves:
+        h.reset()
+    g = torch.Generator(device="cpu").manual_seed(0)
+    for t in range(30):
+        a = (torch.rand((n, 4), generator=g) * 2 - 1).to(DEV)
+        of, rf, _, _ = full.step(a)
+        parts = [h.step(a[r * (n // 2):(r + 1) * (n // 2)]) for r, h in enumerate(halves)]
+        assert torch.equal(of, torch.cat([p[0] for p in parts]))
+        assert torch.equal(rf, torch.cat([p[1] for p in parts]))
+
+
+def test_gpu_full_size_properties():
+    """2^20 envs (the bench workload): invariants that hold at any size, plus demand statistics."""
+    n = 1 << 20
+    env = _env("MAIM", C2, n)
+    env.reset()
+    g = torch.Generator(device="cpu").manual_seed(1)
+    im = torch.tensor(C2["inv_max"], device=DEV, dtype=torch.int32)
+    dsum = torch.zeros((), dtype=torch.float64, device=DEV)
+    dsq = torch.zeros((), dtype=torch.float64, device=DEV)
+    counts = torch.zeros(64, dtype=torch.float64, device=DEV)
+    for t in range(30):
+        a = (torch.rand((n, 4), generator=g) * 2 - 1).to(DEV)
+        inv0 = env.state()
+        obs, rew, done, info = env.step(a, info=True)
+        st = env.state()
+        assert bool(((st["inv"] >= 0) & (st["inv"] <= im)).all())
+        assert bool(((st["backlog"] >= 0) & (st["backlog"] <= im)).all())
+        assert bool(((info["order"] >= 0) & (info["order"] <= im)).all())
+        # balance: ship <= backlog + demand and ship <= inv + acquisition (IM_env.py:315)
+        assert bool((info["ship"] <= inv0["backlog"] + info["demand"]).all())
+        assert bool((info["ship"] <= inv0["inv"] + info["acquisition"]).all())
+        # shared reward is the mean of per-stage profits
+        prof = info["profit"]
+        s = ((((torch.zeros(n, dtype=torch.float64, device=DEV) + prof[:, 0]) + prof[:, 1]) + prof[:, 2]) + prof[:, 3])
+        assert torch.equal(rew, s / 4)
+        assert bool((obs.abs() <= 1.0).all())
+        dcur = info["demand"][:, 0].to(torch.float64)
+        dsum += dcur.sum()
+        dsq += (dcur * dcur).sum()
+        counts += torch.bincount(info["demand"][:, 0].clamp(max=63).long(), minlength=64).double()
+    m = (dsum / (30 * n)).item()
+    v = (dsq / (30 * n)).item() - m * m
+    # demand = min(Poisson(5), inv_max=30): mean/var of Poisson(5) to within sampling error
+    assert abs(m - 5.0) < 0.01 and abs(v - 5.0) < 0.03
+    from scipy.stats import poisson
+    N = 30 * n
+    exp = poisson.pmf(np.arange(64), 5) * N
+    obs_c = counts.cpu().numpy()
+    k = exp > 50
+    chi2 = (((obs_c[k] - exp[k]) ** 2) / exp[k]).sum()
+    assert chi2 < 3 * k.sum(), chi2
+
+
+def test_gpu_errors_and_done():
+    from imenv import ImEnvNativeError
+    env = _env("MAIM", C2, 64)
+    with pytest.raises(ImEnvNativeError):
+        env.step(torch.zeros((64, 4), device=DEV))        # before reset
+    env.reset()
+    for _ in range(30):
+        env.step(torch.zeros((64, 4), device=DEV))
+    with pytest.raises(ImEnvNativeError):
+        env.step(torch.zeros((64, 4), device=DEV))        # past the horizon (reference: IndexError)
