@@ -1,0 +1,270 @@
+#!/usr/bin/env python3
+"""Throughput bench for the north-star path: env-steps/s of the HIP step kernel.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n-envs E] [--no-cpu-baseline]
+
+Workload (BASELINE.json metric "env-steps/sec (whole node), 4-stage x 2^20 envs"):
+MultiAgentInvManagement, 4 stages, MA_1 flags (hyperparams.py:344; constants
+inv_management.py:35-56), shared reward, 2^20 envs per GPU, 30-period episodes,
+in-kernel Philox Poisson(5) demand, float32 actions pre-generated [30][n][4]
+(torch.Generator seed 0) and float32 observations written into a [30][n][4][3]
+rollout buffer, float64 rewards. A "step" = one step() of every env; the reset
+at each episode boundary runs inside the timed region. Multi-GPU: one process
+per GPU (torchrun), each rank owns 2^20 envs at env_offset rank*2^20 (weak
+scaling, no data-path collective; --gather adds the optional per-step RCCL
+all-gather of obs+reward, reported separately).
+
+Prints ONE JSON line on rank 0 (keys per the driver contract), with
+"roofline" (step kernel: algorithmic bytes / HIP-event-timed kernel duration vs
+8 TB/s) and "cpu_baseline" (the oracle port, one env per process, timed on this
+box's host cores before the GPU is touched).
+"""
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "marl-for-im_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+METRIC = "env-steps/sec (whole node), 4-stage × 2^20 envs; % HBM roofline"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E (spec)
+
+C2_CONFIG = dict(num_stages=4, num_periods=30, init_inv=np.ones(4) * 10, inv_target=np.zeros(4),
+                 inv_max=np.ones(4) * 30, price=np.array([5, 4, 3, 2, 1]),
+                 stock_cost=np.array([0.35, 0.3, 0.4, 0.2]), backlog_cost=np.array([0.5, 0.7, 0.6, 0.9]),
+                 delay=np.array([1, 2, 3, 1], dtype=np.int8), demand_dist="poisson", mu=5, seed=52,
+                 standardise_state=True, standardise_actions=True, a=-1, b=1, time_dependency=False,
+                 prev_demand=False, prev_actions=False, prev_length=1, independent=False)
+
+
+def step_bytes(spec):
+    """Algorithmic HBM bytes per env-step of the step kernel, averaged over an episode.
+
+    Steady state: actions 4N (f32) + state 3 fields x 4N read + write
+    + ring 4N read (arrival) + 4N write (departure) + obs 4NF (f32) + reward 8 (f64 shared;
+    8N independent). Exact per-episode average: period 0 reads no state (the initial
+    state is implicit) and node i reads no ring slot while t < delay_i.
+    """
+    N, F, T = spec.num_nodes, spec.num_features, spec.num_periods
+    rew = 8 * N if spec.reward_mode == 2 else 8
+    steady = 4 * N + 24 * N + 8 * N + 4 * N * F + rew
+    skipped = 12 * N + 4 * int(np.minimum(spec.delay, T).sum())   # per episode
+    return steady, steady - skipped / T
+
+
+# ----------------------------------------------------------------- CPU baseline
+def _cpu_worker(args):
+    seconds, seed = args
+    os.environ["OMP_NUM_THREADS"] = "1"
+    from oracle.im_oracle import OracleEnv
+    rs = np.random.RandomState(seed)
+    env = OracleEnv("MAIM", C2_CONFIG, n_envs=1)
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        dem = rs.poisson(5, 30)
+        act = rs.uniform(-1, 1, size=(30, 1, 4)).astype(np.float32).astype(np.float64)
+        env.reset(customer_demand=dem)
+        for t in range(30):
+            env.step(act[t])
+        steps += 30
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            return steps, el
+
+
+def cpu_baseline(seconds=1.5):
+    """Oracle port of the reference step(), one env per process (the reference's own usage:
+    one env per RLlib worker), a pool over this box's cores. Runs in a child interpreter
+    started with BLAS threads pinned to 1 (they must be set before numpy is imported)."""
+    import subprocess
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-only", "--cpu-seconds", str(seconds)],
+                       env=env, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError("cpu baseline failed: " + r.stderr[-2000:])
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def _cpu_baseline_here(seconds):
+    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    ctx = mp.get_context("fork")   # before any GPU call in this process: plain fork, no exec
+    with ctx.Pool(cores) as pool:
+        res = pool.map(_cpu_worker, [(seconds, 100 + i) for i in range(cores)])
+    total = sum(s / e for s, e in res)
+    return dict(value=round(total, 1), unit="env-steps/s", cores=cores, kind="port",
+                sample="oracle/im_oracle.py MAIM 4-stage (C2 constants), 1 env per process, %d processes x "
+                       "%.1f s of whole 30-period episodes each (%d env-steps total), host-fed Poisson(5) demand, "
+                       "BLAS threads 1; per core %.0f env-steps/s" % (cores, seconds, sum(s for s, _ in res),
+                                                                     total / cores))
+
+
+# ----------------------------------------------------------------- PMC traffic
+def pmc_traffic(n_envs):
+    """HBM bytes per step-kernel launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_step_kernel.json, written by tools/pmc_summary.py for this workload), else None."""
+    p = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if int(d.get("n_envs", -1)) == int(n_envs):
+            return float(d["hbm_bytes_per_launch"])
+    except Exception:
+        pass
+    return None
+
+
+# ----------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=60)
+    ap.add_argument("--n-envs", type=int, default=1 << 20, help="envs per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5)
+    ap.add_argument("--gather", action="store_true", help="add the per-step RCCL all-gather of obs+reward")
+    ap.add_argument("--cpu-only", action="store_true", help=argparse.SUPPRESS)
+    args = ap.parse_args()
+    if args.cpu_only:
+        print(json.dumps(_cpu_baseline_here(args.cpu_seconds)))
+        return
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)          # before the GPU is initialised
+
+    import torch
+    import torch.distributed as dist
+    from imenv import VectorInvEnv
+    from imenv import _native as nat
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    n = args.n_envs
+    env = VectorInvEnv("MAIM", C2_CONFIG, n_envs=n, device=dev, env_offset=rank * n)
+    N, F, T = env.N, env.F, env.T
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    actions = torch.rand((T, n, N), generator=g, device=dev, dtype=torch.float32) * 2 - 1
+    obs_buf = torch.empty((T, n, N, F), dtype=torch.float32, device=dev)
+    obs0 = torch.empty((n, N, F), dtype=torch.float32, device=dev)
+    rew_buf = torch.empty((T, n), dtype=torch.float64, device=dev)
+    gat_obs = gat_rew = None
+    if args.gather and world > 1:
+        gat_obs = torch.empty((world * n, N, F), dtype=torch.float32, device=dev)
+        gat_rew = torch.empty((world * n,), dtype=torch.float64, device=dev)
+
+    lib, h = env.lib, env._h
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    a_ptr = [actions[t].data_ptr() for t in range(T)]
+    o_ptr = [obs_buf[t].data_ptr() for t in range(T)]
+    r_ptr = [rew_buf[t].data_ptr() for t in range(T)]
+
+    def run(steps, events=None):
+        for s in range(steps):
+            t = s % T
+            if t == 0:
+                nat.check(lib.imenv_reset(h, None, nat.LAYOUT_DRAW, 0, 0.0, None, -1, obs0.data_ptr(), nat.F32,
+                                          sptr), "imenv_reset")
+            if events is not None:
+                events[s][0].record(stream)
+            rc = lib.imenv_step(h, a_ptr[t], nat.F32, o_ptr[t], nat.F32, r_ptr[t], None, None, sptr)
+            if rc:
+                nat.check(rc, "imenv_step")
+            if events is not None:
+                events[s][1].record(stream)
+            if gat_obs is not None:
+                dist.all_gather_into_tensor(gat_obs, obs_buf[t])
+                dist.all_gather_into_tensor(gat_rew, rew_buf[t])
+
+    # warmup (whole episodes so the timed region starts at a reset)
+    w = ((args.warmup + T - 1) // T) * T
+    run(w)
+    torch.cuda.synchronize(dev)
+    K = args.steps
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run(K, events)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+
+    if world > 1:
+        tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el, kern_ms = tt[0].item(), tt[1].item()
+
+    total_env_steps = world * n * K
+    value = total_env_steps / el
+    b_steady, b_avg = step_bytes(env.spec)
+    achieved_gbs = (b_avg * n) / (kern_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(n)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": w,
+        "ms_per_step": round(el / K * 1e3, 6),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32 state, f64 reward, f32 obs/actions",
+        "data": "synthetic: in-kernel Philox4x32-10 Poisson(5) demand, uniform[-1,1] f32 actions (torch seed 0)",
+        "config": {
+            "workload": "C2 shape at the metric's size: MultiAgentInvManagement 4-stage serial "
+                        "(inv_management.py:35-56 constants, MA_1 flags, shared reward), 2^20 envs per GPU, "
+                        "30-period episodes with the reset inside the timed loop",
+            "n_envs_per_gpu": n, "global_envs": world * n, "num_stages": N, "obs_features": F,
+            "num_periods": T, "parallelism": "env-sharded x%d (one process per GPU, no data-path collective%s)"
+                                             % (world, ", + RCCL all-gather of obs/reward per step" if gat_obs is not None else ""),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved_gbs, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": "imenv_step_kernel<4,0,true>",
+            "kernel_us": round(kern_ms * 1e3, 3),
+            "bytes_per_env_step": round(b_avg, 3),
+            "bytes_per_env_step_steady": b_steady,
+            "bytes_per_launch": round(b_avg * n),
+        },
+        "cpu_baseline": cpu,
+    }
+    if cpu:
+        out["cpu_baseline"]["gpu_over_cpu"] = round(value / cpu["value"], 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
