@@ -44,18 +44,19 @@ C2_CONFIG = dict(num_stages=4, num_periods=30, init_inv=np.ones(4) * 10, inv_tar
                  prev_demand=False, prev_actions=False, prev_length=1, independent=False)
 
 
-def step_bytes(spec):
+def step_bytes(spec, es):
     """Algorithmic HBM bytes per env-step of the step kernel, averaged over an episode.
 
-    Steady state: actions 4N (f32) + state 3 fields x 4N read + write
-    + ring 4N read (arrival) + 4N write (departure) + obs 4NF (f32) + reward 8 (f64 shared;
-    8N independent). Exact per-episode average: period 0 reads no state (the initial
-    state is implicit) and node i reads no ring slot while t < delay_i.
+    es = state element bytes (2: int16 packed state, 4: int32). Steady state:
+    actions 4N (f32) + state 3 fields x N x es read + write + arrivals N x es read +
+    departures N x es write + obs 4NF (f32) + reward 8 (f64 shared; 8N independent).
+    Per-episode average of the MINIMAL bytes: period 0 needs no state read (the initial
+    state is implicit) and node i needs no arrival read while t < delay_i.
     """
     N, F, T = spec.num_nodes, spec.num_features, spec.num_periods
     rew = 8 * N if spec.reward_mode == 2 else 8
-    steady = 4 * N + 24 * N + 8 * N + 4 * N * F + rew
-    skipped = 12 * N + 4 * int(np.minimum(spec.delay, T).sum())   # per episode
+    steady = 4 * N + 6 * N * es + 2 * N * es + 4 * N * F + rew
+    skipped = 3 * N * es + es * int(np.minimum(spec.delay, T).sum())   # per episode
     return steady, steady - skipped / T
 
 
@@ -176,19 +177,27 @@ def main():
     o_ptr = [obs_buf[t].data_ptr() for t in range(T)]
     r_ptr = [rew_buf[t].data_ptr() for t in range(T)]
 
+    # HIP events bracket the step kernel on its own stream at two sampled periods per episode
+    # (t = 7, 22): a timing event pair costs ~7 us of GPU time, so timing every step would slow
+    # the very loop being measured (tools/launch_probe.py).
+    SAMPLE = (7, 22)
+
     def run(steps, events=None):
         for s in range(steps):
             t = s % T
             if t == 0:
                 nat.check(lib.imenv_reset(h, None, nat.LAYOUT_DRAW, 0, 0.0, None, -1, obs0.data_ptr(), nat.F32,
                                           sptr), "imenv_reset")
-            if events is not None:
-                events[s][0].record(stream)
+            ev = events is not None and t in SAMPLE
+            if ev:
+                pair = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                events.append(pair)
+                pair[0].record(stream)
             rc = lib.imenv_step(h, a_ptr[t], nat.F32, o_ptr[t], nat.F32, r_ptr[t], None, None, sptr)
             if rc:
                 nat.check(rc, "imenv_step")
-            if events is not None:
-                events[s][1].record(stream)
+            if ev:
+                pair[1].record(stream)
             if gat_obs is not None:
                 dist.all_gather_into_tensor(gat_obs, obs_buf[t])
                 dist.all_gather_into_tensor(gat_rew, rew_buf[t])
@@ -198,7 +207,7 @@ def main():
     run(w)
     torch.cuda.synchronize(dev)
     K = args.steps
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    events = []
 
     if world > 1:
         dist.barrier()
@@ -218,7 +227,8 @@ def main():
 
     total_env_steps = world * n * K
     value = total_env_steps / el
-    b_steady, b_avg = step_bytes(env.spec)
+    es = env.state_layout()[0]
+    b_steady, b_avg = step_bytes(env.spec, es)
     achieved_gbs = (b_avg * n) / (kern_ms * 1e-3) / 1e9
     traffic = pmc_traffic(n)
     out = {
@@ -249,8 +259,9 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "imenv_step_kernel<4,0,true>",
+            "kernel": "imenv_step_kernel<4,0,true,%s>" % ("short" if env.state_layout()[0] == 2 else "int"),
             "kernel_us": round(kern_ms * 1e3, 3),
+            "kernel_samples": len(events),
             "bytes_per_env_step": round(b_avg, 3),
             "bytes_per_env_step_steady": b_steady,
             "bytes_per_launch": round(b_avg * n),

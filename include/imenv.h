@@ -229,6 +229,10 @@ int imenv_dims(const ImEnv* env, int32_t* num_nodes, int32_t* num_features, int3
  * buffer of capacity `cap`); *len_out receives the table length. */
 int imenv_poisson_table(const ImEnv* env, uint32_t* out, int32_t cap, int32_t* len_out);
 
+/* Packed state layout chosen at create: element bytes (2 = int16 when the
+ * spec's bounds prove every state value fits, else 4), row length per env, arrival-ring depth. */
+int imenv_state_layout(const ImEnv* env, int32_t* elem_bytes, int32_t* row_len, int32_t* ring_depth);
+
 void imenv_destroy(ImEnv* env);
 
 const char* imenv_last_error(void);

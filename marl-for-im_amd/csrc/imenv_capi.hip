@@ -1,0 +1,590 @@
+// imenv_capi.hip — host side of the C ABI in include/imenv.h: spec validation and derivation,
+// buffer ownership, the reset / state-unpack kernels and step-kernel dispatch.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "imenv_device.h"
+
+using imenv::LaunchCfg;
+using imenv::SpecDev;
+using imenv::StepArgs;
+
+namespace {
+
+// ------------------------------------------------------------------ reset kernel
+// Period-0 observation (IM_env.py:221-229): inv = init_inv, everything else 0 — the same
+// [N][F] row for every env (host-built template), written with 16-B stores. It also clears the
+// split-guard flags and advances the device-resident episode counter (the Philox counter word):
+// set to `episode` if >= 0, else incremented, so a captured reset+steps graph draws fresh demand
+// on every replay.
+__global__ void __launch_bounds__(256) imenv_reset_kernel(const SpecDev* __restrict__ sp, void* obs, int obs_f64,
+                                                          int64_t n, uint32_t* episode_word, int64_t episode,
+                                                          uint32_t* err, uint32_t* err_any) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *episode_word = episode >= 0 ? (uint32_t)episode : *episode_word + 1u;
+    *err_any = 0u;
+  }
+  const int row = sp->s.num_nodes * sp->s.num_features;
+  const int64_t total = n * row;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t q = q0; q < n; q += stride) err[q] = 0u;
+  if (!obs_f64 && (row & 3) == 0) {
+    const int r4 = row >> 2;
+    float4* o4 = static_cast<float4*>(obs);
+    const float4* tpl = reinterpret_cast<const float4*>(sp->reset_f32);
+    for (int64_t q = q0; q < total / 4; q += stride) o4[q] = tpl[q % r4];
+  } else if (obs_f64 && (row & 1) == 0) {
+    const int r2 = row >> 1;
+    double2* o2 = static_cast<double2*>(obs);
+    const double2* tpl = reinterpret_cast<const double2*>(sp->reset_f64);
+    for (int64_t q = q0; q < total / 2; q += stride) o2[q] = tpl[q % r2];
+  } else {
+    for (int64_t q = q0; q < total; q += stride) {
+      if (obs_f64) static_cast<double*>(obs)[q] = sp->reset_f64[q % row];
+      else static_cast<float*>(obs)[q] = sp->reset_f32[q % row];
+    }
+  }
+}
+
+// packed [n][np] state rows -> int32 [N][n] SoA (imenv_get_state)
+template <typename ST>
+__global__ void __launch_bounds__(256) imenv_unpack_kernel(const ST* __restrict__ src, int32_t* __restrict__ dst,
+                                                           int64_t n, int np, int N) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  for (int i = 0; i < N; ++i) dst[i * n + e] = (int32_t)src[e * np + i];
+}
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                                    \
+  do {                                                                                               \
+    hipError_t _e = (x);                                                                             \
+    if (_e != hipSuccess) return fail(IMENV_E_HIP, std::string(#x ": ") + hipGetErrorString(_e));    \
+  } while (0)
+
+uint64_t prob_thr32(double p) {
+  double v = std::ceil(p * 4294967296.0);
+  if (v < 0) v = 0;
+  if (v > 4294967296.0) v = 4294967296.0;
+  return (uint64_t)v;
+}
+
+// Host twin of obs_map: the same IEEE double expression, so table entries are bit-identical
+// to what the device would compute (both built with -ffp-contract=off).
+double host_obs_map(int mode, double v, double a, double bma, double den, double clip) {
+  if (mode == IMENV_OBS_RAW) return v;
+  if (mode == IMENV_OBS_SCALED) return a + (v * bma) / den;
+  if (mode == IMENV_OBS_CLAMP_SCALED) return a + (std::fmin(v, clip) * bma) / den;
+  return 0.0;
+}
+
+// Largest demand a node can see in one period: retailers are capped at inv_max
+// (IM_env.py:306), other nodes receive at most the sum of their children's order_max.
+int64_t demand_bound(const ImEnvSpec& s, int i) {
+  if (s.retailer_slot[i] >= 0) return s.inv_max[i];
+  int64_t b = 0;
+  for (int c = 0; c < s.num_nodes; ++c)
+    if (s.demand_parent[c] == i) b += s.order_max[c];
+  return b;
+}
+
+// Observation lookup tables: for every scaled group and node, the exact value for each integer
+// raw value the state can take (bounded by the capacities); values outside fall back to the
+// in-kernel expression. Also the period-0 row shared by every env.
+void build_obs_tables(SpecDev& d, std::vector<float>& l32, std::vector<double>& l64) {
+  const ImEnvSpec& s = d.s;
+  const int N = s.num_nodes;
+  const double a = s.a, bma = s.b - s.a;
+  l32.clear();
+  l64.clear();
+  for (int g = 0; g < IMENV_NUM_GROUPS; ++g) {
+    for (int i = 0; i < IMENV_MAX_NODES; ++i) { d.lut_off[g][i] = 0; d.lut_max[g][i] = -1; }
+    const int mode = s.group_mode[g];
+    if (mode != IMENV_OBS_SCALED && mode != IMENV_OBS_CLAMP_SCALED) continue;
+    for (int i = 0; i < N; ++i) {
+      int64_t vmax = 0;
+      switch (g) {
+        case IMENV_G_INV: case IMENV_G_ORDER_U: vmax = s.inv_max[i]; break;
+        case IMENV_G_BACKLOG: vmax = s.backlog_cap[i] >= 0 ? s.backlog_cap[i] : s.inv_max[i]; break;
+        case IMENV_G_DEMAND_HIST: vmax = demand_bound(s, i); break;
+        case IMENV_G_ORDER_HIST: vmax = s.order_max[i]; break;
+        case IMENV_G_TRANSIT:
+          vmax = mode == IMENV_OBS_CLAMP_SCALED ? (int64_t)std::fmin(s.group_clip[g][i], 4096.0)
+                                                : (s.parent[i] >= 0 ? s.inv_max[s.parent[i]] : s.order_max[i]);
+          break;
+        case IMENV_G_NODE_ID: vmax = N; break;
+        default: vmax = -1;
+      }
+      if (vmax > 4096) vmax = 4096;
+      if (vmax < 0) continue;
+      d.lut_off[g][i] = (int32_t)l64.size();
+      d.lut_max[g][i] = (int32_t)vmax;
+      for (int64_t v = 0; v <= vmax; ++v) {
+        const double o = host_obs_map(mode, (double)v, a, bma, s.group_den[g][i], s.group_clip[g][i]);
+        l64.push_back(o);
+        l32.push_back((float)o);
+      }
+    }
+  }
+  const int F = s.num_features;
+  for (int i = 0; i < N; ++i) {
+    for (int f = 0; f < F; ++f) {
+      const int g = s.feat_group[f];
+      double v = 0.0;
+      if (g == IMENV_G_INV) v = s.init_inv[i];
+      else if (g == IMENV_G_NODE_ID) v = i;
+      const double o = host_obs_map(s.group_mode[g], v, a, bma, s.group_den[g][i], s.group_clip[g][i]);
+      d.reset_f64[i * F + f] = o;
+      d.reset_f32[i * F + f] = (float)o;
+    }
+  }
+}
+
+// 1/x when x is a (signed) power of two, so that y / x == y * (1/x) exactly; else 0.
+double exact_reciprocal(double x) {
+  if (!(x != 0.0) || !std::isfinite(x)) return 0.0;
+  int ex = 0;
+  const double m = std::frexp(std::fabs(x), &ex);
+  if (m != 0.5) return 0.0;
+  return 1.0 / x;
+}
+
+// Can every value held in the packed state (inventory, backlog, unfulfilled orders, shipments in
+// transit, demand / order history) be proven to fit int16? Backlog grows by at most one period's
+// demand per period when uncapped; a shipment is at most backlog + demand, plus the split's
+// overshoot of (children - 1) units (its inner loop does not re-check the remaining amount).
+bool state_fits_int16(const ImEnvSpec& s) {
+  const int N = s.num_nodes;
+  int64_t B = 0;
+  auto upd = [&](int64_t v) { if (v > B) B = v; };
+  for (int i = 0; i < N; ++i) {
+    const int64_t dm = demand_bound(s, i);
+    const int64_t blb = s.backlog_cap[i] >= 0 ? s.backlog_cap[i] : (int64_t)s.num_periods * dm;
+    upd(s.inv_max[i]); upd(s.init_inv[i]); upd(blb); upd(dm); upd(s.order_max[i]);
+    const int64_t shipb = blb + dm + IMENV_MAX_CHILDREN;
+    upd(shipb);
+  }
+  return B <= 32767;
+}
+
+int validate_and_derive(const ImEnvSpec& s, SpecDev& d, int& maxc) {
+  if (s.abi_version != IMENV_ABI_VERSION) return fail(IMENV_E_INVALID, "abi_version mismatch");
+  const int N = s.num_nodes;
+  if (N < 1 || N > IMENV_MAX_NODES) return fail(IMENV_E_INVALID, "num_nodes out of range");
+  if (s.num_periods < 1 || s.num_periods > IMENV_MAX_PERIODS) return fail(IMENV_E_INVALID, "num_periods out of range");
+  std::memset(&d, 0, sizeof(d));
+  d.s = s;
+  int roots = 0;
+  d.factory = -1;
+  d.dmax = 1;
+  for (int i = 0; i < N; ++i) {
+    if (s.parent[i] < 0) { ++roots; d.factory = i; }
+    else if (s.parent[i] >= N || s.parent[i] == i) return fail(IMENV_E_INVALID, "bad parent index");
+    if (s.delay[i] < 1)
+      return fail(IMENV_E_UNSUPPORTED, "delay must be >= 1 in this build (delay 0 is a degenerate lead time)");
+    if (s.delay[i] > IMENV_MAX_DELAY) return fail(IMENV_E_INVALID, "delay too large");
+    if (s.delay[i] > d.dmax) d.dmax = s.delay[i];
+    if (s.inv_max[i] < 0 || s.order_max[i] < 0 || s.init_inv[i] < 0) return fail(IMENV_E_INVALID, "negative capacity");
+    if (s.num_children[i] < 0 || s.num_children[i] > IMENV_MAX_CHILDREN)
+      return fail(IMENV_E_UNSUPPORTED, "too many children");
+  }
+  if (roots != 1) return fail(IMENV_E_INVALID, "topology needs exactly one factory (parent = -1)");
+  maxc = 0;
+  d.num_split = 0;
+  for (int i = 0; i < N; ++i) { d.split_child[i] = 0; d.single_parent[i] = -1; }
+  for (int p = 0; p < N; ++p) {
+    const int m = s.num_children[p];
+    for (int k = 0; k < m; ++k) {
+      const int c = s.children[p][k];
+      if (c < 0 || c >= N || s.parent[c] != p) return fail(IMENV_E_INVALID, "children/parent mismatch");
+    }
+    if (m == 1) d.single_parent[s.children[p][0]] = p;
+    if (m > 1) {
+      d.split_node[d.num_split++] = p;
+      if (m > maxc) maxc = m;
+      for (int k = 0; k < m; ++k) d.split_child[s.children[p][k]] = 1;
+    }
+  }
+  int nret = 0;
+  for (int i = 0; i < N; ++i) {
+    if (s.retailer_slot[i] >= 0) {
+      ++nret;
+      if (s.retailer_slot[i] >= s.num_retailers) return fail(IMENV_E_INVALID, "retailer_slot out of range");
+    }
+    if (s.demand_parent[i] >= N) return fail(IMENV_E_INVALID, "bad demand_parent");
+  }
+  if (nret != s.num_retailers || nret < 1) return fail(IMENV_E_INVALID, "retailer count mismatch");
+  if (s.num_features < 1 || s.num_features > IMENV_MAX_FEATURES) return fail(IMENV_E_INVALID, "num_features out of range");
+  if (s.prev_length < 1 || s.prev_length > IMENV_MAX_HIST) return fail(IMENV_E_INVALID, "prev_length out of range");
+  for (int f = 0; f < s.num_features; ++f) {
+    if (s.feat_group[f] < 0 || s.feat_group[f] >= IMENV_NUM_GROUPS) return fail(IMENV_E_INVALID, "bad feature group");
+    if (s.feat_index[f] < 0) return fail(IMENV_E_INVALID, "bad feature index");
+    if ((s.feat_group[f] == IMENV_G_DEMAND_HIST || s.feat_group[f] == IMENV_G_ORDER_HIST) &&
+        s.feat_index[f] >= s.prev_length)
+      return fail(IMENV_E_INVALID, "history feature index >= prev_length");
+    if (s.feat_group[f] == IMENV_G_TRANSIT && s.feat_index[f] >= d.dmax)
+      return fail(IMENV_E_INVALID, "transit feature index >= max delay");
+  }
+  for (int g = 0; g < IMENV_NUM_GROUPS; ++g)
+    if (s.group_mode[g] < IMENV_OBS_ZERO || s.group_mode[g] > IMENV_OBS_CLAMP_SCALED)
+      return fail(IMENV_E_INVALID, "bad group mode");
+  if (s.decode_mode != IMENV_DECODE_CLIP_ROUND && s.decode_mode != IMENV_DECODE_ROUND_CLIP)
+    return fail(IMENV_E_INVALID, "bad decode_mode");
+  if (s.reward_mode < IMENV_REWARD_SUM || s.reward_mode > IMENV_REWARD_INDEPENDENT)
+    return fail(IMENV_E_INVALID, "bad reward_mode");
+  if (s.standardise_actions && !(s.b - s.a != 0.0)) return fail(IMENV_E_INVALID, "a == b");
+  d.table_len = 0;
+  if (s.demand_dist == IMENV_DEMAND_POISSON) {
+    // thr[k] = ceil(CDF(k) * 2^32) by the pmf recurrence (oracle/philox.py:poisson_thresholds)
+    const double mu = s.poisson_mu;
+    if (!(mu > 0.0)) return fail(IMENV_E_INVALID, "Poisson mean must be positive");
+    double p = std::exp(-mu), cdf = 0.0;
+    int k = 0;
+    for (;;) {
+      cdf += p;
+      const double tv = std::ceil(cdf * 4294967296.0);
+      if (tv >= 4294967296.0) break;
+      if (k >= IMENV_TABLE_MAX) return fail(IMENV_E_UNSUPPORTED, "Poisson mean too large for the inversion table");
+      d.table[k] = (uint32_t)tv;
+      ++k;
+      p = p * mu / (double)k;
+    }
+    d.table_len = k;
+  } else if (s.demand_dist == IMENV_DEMAND_UNIFORM) {
+    if (s.uniform_low >= s.uniform_high)
+      return fail(IMENV_E_INVALID, "Lower bound cannot be larger than upper bound");
+  } else if (s.demand_dist != IMENV_DEMAND_CUSTOM) {
+    return fail(IMENV_E_INVALID, "Unrecognised, Distribution Not Implemented");
+  }
+  d.st16 = state_fits_int16(s) ? 1 : 0;
+  d.inv_bma = exact_reciprocal(s.b - s.a);
+  d.inv_n = exact_reciprocal((double)N);
+  d.np = d.st16 ? ((N + 1) & ~1) : N;
+  return IMENV_OK;
+}
+
+template <typename T>
+int alloc(T** p, size_t count) {
+  if (count == 0) { *p = nullptr; return IMENV_OK; }
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)));
+  return IMENV_OK;
+}
+
+bool is_base_obs(const ImEnvSpec& s) {
+  return s.num_features == 3 && s.feat_group[0] == IMENV_G_INV && s.feat_group[1] == IMENV_G_BACKLOG &&
+         s.feat_group[2] == IMENV_G_ORDER_U;
+}
+
+}  // namespace
+
+// ==================================================================== handle
+struct ImEnv {
+  SpecDev host;        // host copy of the device spec
+  SpecDev* d_spec = nullptr;
+  int device = 0;
+  int64_t n = 0;
+  int64_t env_offset = 0;
+  int maxc = 0;
+  size_t es = 4;       // state element size (2 or 4)
+  void *d_inv = nullptr, *d_bl = nullptr, *d_ou = nullptr, *d_ring = nullptr, *d_hist_d = nullptr, *d_hist_o = nullptr;
+  int32_t *d_carry = nullptr, *d_bto = nullptr, *d_demand = nullptr;
+  double* d_delay_u = nullptr;
+  float* d_lut32 = nullptr;
+  double* d_lut64 = nullptr;
+  std::vector<float> lut32;
+  std::vector<double> lut64;
+  uint32_t *d_err = nullptr, *d_err_any = nullptr;
+  uint32_t* d_episode = nullptr;
+  int t = 0;
+  bool reset_done = false;
+  bool noisy_delay = false;
+  double noisy_thr = 0.0;
+  bool have_delay_u = false;
+  int demand_layout = IMENV_LAYOUT_DRAW;
+  size_t demand_cap = 0;
+};
+
+extern "C" {
+
+int imenv_abi_version(void) { return IMENV_ABI_VERSION; }
+
+int64_t imenv_spec_size(void) { return (int64_t)sizeof(ImEnvSpec); }
+
+const char* imenv_last_error(void) { return g_err.c_str(); }
+
+void imenv_destroy(ImEnv* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  void* ptrs[] = {h->d_spec, h->d_inv, h->d_bl, h->d_ou, h->d_ring, h->d_carry, h->d_bto, h->d_hist_d,
+                  h->d_hist_o, h->d_demand, h->d_delay_u, h->d_err, h->d_err_any, h->d_lut32, h->d_lut64,
+                  h->d_episode};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  delete h;
+}
+
+int imenv_create(const ImEnvSpec* spec, int64_t n_envs, int64_t env_offset, int device, ImEnv** out) {
+  if (!spec || !out) return fail(IMENV_E_INVALID, "null argument");
+  *out = nullptr;
+  if (n_envs < 1 || n_envs > (int64_t(1) << 31)) return fail(IMENV_E_INVALID, "n_envs out of range");
+  if (env_offset < 0 || env_offset + n_envs > (int64_t(1) << 32)) return fail(IMENV_E_INVALID, "env ids must fit 32 bits");
+  ImEnv* h = new ImEnv();
+  int rc = validate_and_derive(*spec, h->host, h->maxc);
+  if (rc != IMENV_OK) { delete h; return rc; }
+  h->device = device;
+  h->n = n_envs;
+  h->env_offset = env_offset;
+  h->noisy_delay = spec->noisy_delay != 0;
+  h->noisy_thr = spec->noisy_delay_threshold;
+  h->es = h->host.st16 ? 2 : 4;
+  const ImEnvSpec& s = *spec;
+  const size_t n = n_envs, np = h->host.np, rowb = n * np * h->es;
+  bool uses_hist = false;
+  for (int f = 0; f < s.num_features; ++f)
+    if (s.feat_group[f] == IMENV_G_DEMAND_HIST || s.feat_group[f] == IMENV_G_ORDER_HIST) uses_hist = true;
+  hipError_t he = hipSetDevice(device);
+  if (he != hipSuccess) { delete h; return fail(IMENV_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(he)); }
+  char **inv = reinterpret_cast<char**>(&h->d_inv), **bl = reinterpret_cast<char**>(&h->d_bl),
+       **ou = reinterpret_cast<char**>(&h->d_ou), **ring = reinterpret_cast<char**>(&h->d_ring);
+  if ((rc = alloc(&h->d_spec, 1)) || (rc = alloc(inv, rowb)) || (rc = alloc(bl, rowb)) || (rc = alloc(ou, rowb)) ||
+      (rc = alloc(ring, rowb * h->host.dmax)) || (rc = alloc(&h->d_carry, n * np)) ||
+      (rc = alloc(&h->d_bto, h->maxc > 0 ? n * np : 0)) || (rc = alloc(&h->d_err, n)) ||
+      (rc = alloc(&h->d_err_any, 1)) || (rc = alloc(&h->d_episode, 1))) {
+    imenv_destroy(h);
+    return rc;
+  }
+  if (uses_hist) {
+    char **hd = reinterpret_cast<char**>(&h->d_hist_d), **ho = reinterpret_cast<char**>(&h->d_hist_o);
+    if ((rc = alloc(hd, rowb * s.prev_length)) || (rc = alloc(ho, rowb * s.prev_length))) {
+      imenv_destroy(h);
+      return rc;
+    }
+  }
+  build_obs_tables(h->host, h->lut32, h->lut64);
+  if ((rc = alloc(&h->d_lut32, h->lut32.size() + 1)) || (rc = alloc(&h->d_lut64, h->lut64.size() + 1))) {
+    imenv_destroy(h);
+    return rc;
+  }
+  he = hipMemcpy(h->d_spec, &h->host, sizeof(SpecDev), hipMemcpyHostToDevice);
+  if (he == hipSuccess && !h->lut32.empty())
+    he = hipMemcpy(h->d_lut32, h->lut32.data(), h->lut32.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (he == hipSuccess && !h->lut64.empty())
+    he = hipMemcpy(h->d_lut64, h->lut64.data(), h->lut64.size() * sizeof(double), hipMemcpyHostToDevice);
+  if (he == hipSuccess) he = hipMemset(h->d_err, 0, n * sizeof(uint32_t));
+  if (he == hipSuccess) he = hipMemset(h->d_err_any, 0, sizeof(uint32_t));
+  if (he == hipSuccess) he = hipMemset(h->d_episode, 0xFF, sizeof(uint32_t));   // first auto reset -> 0
+  if (he != hipSuccess) { imenv_destroy(h); return fail(IMENV_E_HIP, std::string("init copy: ") + hipGetErrorString(he)); }
+  *out = h;
+  return IMENV_OK;
+}
+
+int imenv_reset(ImEnv* h, const int32_t* demand, int demand_layout, int noisy_delay, double noisy_delay_threshold,
+                const double* delay_uniforms, int64_t episode, void* obs, int obs_dtype, void* stream) {
+  if (!h || !obs) return fail(IMENV_E_INVALID, "null argument");
+  if (obs_dtype != IMENV_F32 && obs_dtype != IMENV_F64) return fail(IMENV_E_INVALID, "bad obs dtype");
+  const ImEnvSpec& s = h->host.s;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  HIPCHK(hipSetDevice(h->device));
+  const size_t T = s.num_periods, R = s.num_retailers, n = h->n, N = s.num_nodes;
+  if (demand_layout == IMENV_LAYOUT_DRAW) {
+    if (demand) return fail(IMENV_E_INVALID, "IMENV_LAYOUT_DRAW takes no demand table");
+    if (s.demand_dist != IMENV_DEMAND_POISSON && s.demand_dist != IMENV_DEMAND_UNIFORM)
+      return fail(IMENV_E_INVALID, "custom demand needs a table (IMENV_LAYOUT_BROADCAST)");
+  } else if (demand_layout == IMENV_LAYOUT_PER_ENV || demand_layout == IMENV_LAYOUT_BROADCAST) {
+    if (!demand) return fail(IMENV_E_INVALID, "missing customer-demand table");
+    const size_t cnt = (demand_layout == IMENV_LAYOUT_PER_ENV) ? T * R * n : T * R;
+    if (h->demand_cap < cnt) {
+      if (h->d_demand) { HIPCHK(hipStreamSynchronize(st)); HIPCHK(hipFree(h->d_demand)); h->d_demand = nullptr; }
+      int rc = alloc(&h->d_demand, cnt);
+      if (rc) return rc;
+      h->demand_cap = cnt;
+    }
+    HIPCHK(hipMemcpyAsync(h->d_demand, demand, cnt * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+  } else {
+    return fail(IMENV_E_INVALID, "bad demand_layout");
+  }
+  h->demand_layout = demand_layout;
+  if (noisy_delay) {             // IM_env.py:180-182: latched until the env is rebuilt
+    h->noisy_delay = true;
+    h->noisy_thr = noisy_delay_threshold;
+  }
+  h->have_delay_u = false;
+  if (delay_uniforms) {
+    if (!h->d_delay_u) {
+      int rc = alloc(&h->d_delay_u, T * N * n);
+      if (rc) return rc;
+    }
+    HIPCHK(hipMemcpyAsync(h->d_delay_u, delay_uniforms, T * N * n * sizeof(double), hipMemcpyDeviceToDevice, st));
+    h->have_delay_u = true;
+  }
+  h->t = 0;
+  h->reset_done = true;
+  int64_t blocks = ((int64_t)n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(imenv_reset_kernel, dim3((unsigned)blocks), dim3(256), 0, st, h->d_spec, obs,
+                     obs_dtype == IMENV_F64 ? 1 : 0, (int64_t)n, h->d_episode, episode, h->d_err, h->d_err_any);
+  HIPCHK(hipGetLastError());
+  return IMENV_OK;
+}
+
+int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int obs_dtype, double* reward,
+               const ImEnvInfo* info, int32_t* done_out, void* stream) {
+  if (!h || !actions || !obs || !reward) return fail(IMENV_E_INVALID, "null argument");
+  if (!h->reset_done) return fail(IMENV_E_NOT_RESET, "step() before reset()");
+  const ImEnvSpec& s = h->host.s;
+  if (h->t >= s.num_periods) return fail(IMENV_E_DONE, "step() past num_periods (episode is done; call reset)");
+  if (action_dtype != IMENV_F32 && action_dtype != IMENV_F64) return fail(IMENV_E_INVALID, "bad action dtype");
+  if (obs_dtype != IMENV_F32 && obs_dtype != IMENV_F64) return fail(IMENV_E_INVALID, "bad obs dtype");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  HIPCHK(hipSetDevice(h->device));
+  StepArgs A;
+  std::memset(&A, 0, sizeof(A));
+  A.actions = actions;
+  A.obs = obs;
+  A.reward = reward;
+  A.inv = h->d_inv; A.bl = h->d_bl; A.ou = h->d_ou;
+  A.ring = h->d_ring; A.carry = h->d_carry; A.bto = h->d_bto;
+  A.hist_d = h->d_hist_d; A.hist_o = h->d_hist_o;
+  A.demand = h->d_demand;
+  A.delay_u = h->have_delay_u ? h->d_delay_u : nullptr;
+  A.err = h->d_err; A.err_any = h->d_err_any;
+  if (info) {
+    A.i_order = info->order; A.i_demand = info->demand; A.i_acq = info->acquisition; A.i_ship = info->ship;
+    A.i_profit = info->profit; A.i_ship_to = info->ship_to; A.i_bto = info->backlog_to;
+    if (!A.i_order && (A.i_demand || A.i_acq || A.i_ship || A.i_profit || A.i_ship_to || A.i_bto))
+      return fail(IMENV_E_INVALID, "info.order is required when any other info field is requested");
+  }
+  A.lut32 = h->d_lut32;
+  A.lut64 = h->d_lut64;
+  A.episode = h->d_episode;
+  A.n = h->n;
+  A.env_offset = (uint32_t)h->env_offset;
+  A.t = h->t;
+  A.action_f64 = action_dtype == IMENV_F64;
+  A.obs_f64 = obs_dtype == IMENV_F64;
+  A.demand_layout = h->demand_layout;
+  A.noisy_demand = (s.noisy_demand && h->demand_layout != IMENV_LAYOUT_PER_ENV) ? 1 : 0;
+  A.noisy_delay = h->noisy_delay ? 1 : 0;
+  A.noisy_delay_thr = h->noisy_thr;
+  A.noisy_delay_thr32 = prob_thr32(h->noisy_thr);
+  A.noisy_demand_thr32 = prob_thr32(s.noisy_demand_threshold);
+  const int D = h->host.dmax;
+  A.arr_row = h->t % D;
+  for (int i = 0; i < s.num_nodes; ++i) A.dep_row[i] = (h->t + s.delay[i]) % D;
+  LaunchCfg c;
+  c.mc = h->maxc;
+  c.base = is_base_obs(s);
+  c.st16 = h->host.st16 != 0;
+  c.grid = (unsigned)((h->n + 255) / 256);
+  c.stream = st;
+  const int N = s.num_nodes;
+  switch (N) {   // exact kernels for N <= 8, padded NT = 16 above
+    case 1: imenv::launch_step_nt<1>(c, h->d_spec, A); break;
+    case 2: imenv::launch_step_nt<2>(c, h->d_spec, A); break;
+    case 3: imenv::launch_step_nt<3>(c, h->d_spec, A); break;
+    case 4: imenv::launch_step_nt<4>(c, h->d_spec, A); break;
+    case 5: imenv::launch_step_nt<5>(c, h->d_spec, A); break;
+    case 6: imenv::launch_step_nt<6>(c, h->d_spec, A); break;
+    case 7: imenv::launch_step_nt<7>(c, h->d_spec, A); break;
+    case 8: imenv::launch_step_nt<8>(c, h->d_spec, A); break;
+    default: imenv::launch_step_nt<16>(c, h->d_spec, A); break;
+  }
+  HIPCHK(hipGetLastError());
+  h->t += 1;
+  if (done_out) *done_out = h->t >= s.num_periods ? 1 : 0;
+  return IMENV_OK;
+}
+
+int imenv_get_state(ImEnv* h, int32_t* inv, int32_t* backlog, int32_t* order_u, int32_t* period, void* stream) {
+  if (!h) return fail(IMENV_E_INVALID, "null handle");
+  const ImEnvSpec& s = h->host.s;
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const size_t bytes = (size_t)s.num_nodes * h->n * sizeof(int32_t);
+  if (h->t == 0) {
+    // period-0 state is implicit in the step kernel; materialise it for the caller
+    if (inv) {
+      std::vector<int32_t> tmp((size_t)s.num_nodes * h->n);
+      for (int i = 0; i < s.num_nodes; ++i)
+        for (int64_t e = 0; e < h->n; ++e) tmp[(size_t)i * h->n + e] = s.init_inv[i];
+      HIPCHK(hipMemcpyAsync(inv, tmp.data(), bytes, hipMemcpyHostToDevice, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    if (backlog) HIPCHK(hipMemsetAsync(backlog, 0, bytes, st));
+    if (order_u) HIPCHK(hipMemsetAsync(order_u, 0, bytes, st));
+  } else {
+    const unsigned grid = (unsigned)((h->n + 255) / 256);
+    void* src[3] = {h->d_inv, h->d_bl, h->d_ou};
+    int32_t* dst[3] = {inv, backlog, order_u};
+    for (int k = 0; k < 3; ++k) {
+      if (!dst[k]) continue;
+      if (h->host.st16)
+        hipLaunchKernelGGL(imenv_unpack_kernel<int16_t>, dim3(grid), dim3(256), 0, st,
+                           static_cast<const int16_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes);
+      else
+        hipLaunchKernelGGL(imenv_unpack_kernel<int32_t>, dim3(grid), dim3(256), 0, st,
+                           static_cast<const int32_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes);
+    }
+    HIPCHK(hipGetLastError());
+  }
+  if (period) *period = h->t;
+  return IMENV_OK;
+}
+
+int imenv_get_errors(ImEnv* h, uint32_t* flags, uint32_t* any_out, void* stream) {
+  if (!h) return fail(IMENV_E_INVALID, "null handle");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (flags) HIPCHK(hipMemcpyAsync(flags, h->d_err, h->n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+  if (any_out) {
+    uint32_t v = 0;
+    HIPCHK(hipMemcpyAsync(&v, h->d_err_any, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *any_out = v;
+  }
+  return IMENV_OK;
+}
+
+int imenv_dims(const ImEnv* h, int32_t* num_nodes, int32_t* num_features, int32_t* num_retailers,
+               int32_t* num_periods) {
+  if (!h) return fail(IMENV_E_INVALID, "null handle");
+  const ImEnvSpec& s = h->host.s;
+  if (num_nodes) *num_nodes = s.num_nodes;
+  if (num_features) *num_features = s.num_features;
+  if (num_retailers) *num_retailers = s.num_retailers;
+  if (num_periods) *num_periods = s.num_periods;
+  return IMENV_OK;
+}
+
+int imenv_poisson_table(const ImEnv* h, uint32_t* out, int32_t cap, int32_t* len_out) {
+  if (!h) return fail(IMENV_E_INVALID, "null handle");
+  if (len_out) *len_out = h->host.table_len;
+  if (out) {
+    const int m = cap < h->host.table_len ? cap : h->host.table_len;
+    for (int k = 0; k < m; ++k) out[k] = h->host.table[k];
+  }
+  return IMENV_OK;
+}
+
+int imenv_state_layout(const ImEnv* h, int32_t* elem_bytes, int32_t* row_len, int32_t* ring_depth) {
+  if (!h) return fail(IMENV_E_INVALID, "null handle");
+  if (elem_bytes) *elem_bytes = (int32_t)h->es;
+  if (row_len) *row_len = h->host.np;
+  if (ring_depth) *ring_depth = h->host.dmax;
+  return IMENV_OK;
+}
+
+}  // extern "C"

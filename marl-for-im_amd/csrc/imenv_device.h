@@ -1,0 +1,862 @@
+// imenv_device.h — device-side data structures and the fused step kernel body (gfx950).
+//
+// One kernel advances every env by one period: order decode (rev_scale + round/clip),
+// demand assembly (host-fed or in-kernel Philox), lead-time arrivals, shipment, the
+// divergent per-edge split, backlog / order_u / inventory balance, per-node profit and
+// reward, and the next observation. It restates environments/IM_env.py:287-456,
+// MAIM_env.py:330-519, IM_div_env.py:361-645 and MAIM_div_env.py:441-739 (every quirk
+// listed in SURVEY.md §8a), batched over envs, one thread per env.
+//
+// The body is a template over a spec policy P:
+//   DynSpec<NT, MC, BASE, ST>  reads the spec from device memory (ahead-of-time kernels, any spec)
+//   JitSpec (generated)        every spec value is a constexpr: hipRTC compiles one kernel per
+//                              spec with all constants folded into immediates (imenv_jit.cpp)
+//
+// HBM layout. ST = int16 when the spec's bounds prove every value fits, else
+// int32. NP = row length in ST elements (N, rounded up to even for int16 so rows are
+// 4-byte aligned).
+//   inv, backlog, order_u   [n][NP] ST      one packed row per env: 8 B per lane for N=4 int16
+//   ring (arrivals)         [D][n][NP] ST   time-major: row (t mod D) holds what arrives at t
+//                                           for every node (ONE vector load per env); node i's
+//                                           departure goes to row (t + d_i) mod D, lane i
+//   hist_d / hist_o         [L][n][NP] ST   demand / order history rows (prev_* observations)
+//   backlog_to, carry       [n][NP] int32   split state (trees) / noisy-delay carry
+//   actions [n][N] f32|f64, obs [n][N][F] f32|f64, reward [n] or [n][N] f64 (policy layout)
+// Build: --offload-arch=gfx950 -O3 -ffp-contract=off (no FMA contraction, IEEE division:
+// float64 rewards/obs are bit-exact with NumPy).
+#pragma once
+
+#ifndef __HIPCC_RTC__
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+#else
+typedef signed char int8_t;
+typedef short int16_t;
+typedef unsigned short uint16_t;
+typedef int int32_t;
+typedef unsigned int uint32_t;
+typedef long long int64_t;
+typedef unsigned long long uint64_t;
+#define INT_MAX 2147483647
+#endif
+
+#include "imenv.h"
+
+#define IMENV_TABLE_MAX 1024
+
+namespace imenv {
+
+struct SpecDev {
+  ImEnvSpec s;
+  int32_t num_split;                        // nodes with > 1 child, ascending
+  int32_t split_node[IMENV_MAX_NODES];
+  int32_t split_child[IMENV_MAX_NODES];     // 1 if node's parent splits its shipment
+  int32_t single_parent[IMENV_MAX_NODES];   // parent if it has exactly one child, else -1
+  int32_t factory;
+  int32_t dmax;                             // ring depth D = max delay
+  int32_t np;                               // packed row length (elements)
+  int32_t st16;                             // state element type: 1 = int16, 0 = int32
+  int32_t table_len;
+  uint32_t table[IMENV_TABLE_MAX];          // Poisson inversion thresholds
+  // observation lookup: value of group g, node i for raw v in [0, lut_max] at lut[lut_off + v]
+  int32_t lut_off[IMENV_NUM_GROUPS][IMENV_MAX_NODES];
+  int32_t lut_max[IMENV_NUM_GROUPS][IMENV_MAX_NODES];   // -1: not tabulated
+  // period-0 observation row (the same for every env)
+  alignas(16) float reset_f32[IMENV_MAX_NODES * IMENV_MAX_FEATURES];
+  alignas(16) double reset_f64[IMENV_MAX_NODES * IMENV_MAX_FEATURES];
+  double inv_bma;                           // 1/(b - a) when b - a is a power of two, else 0
+  double inv_n;                             // 1/N when N is a power of two, else 0
+};
+
+struct StepArgs {
+  const void* actions;
+  void* obs;
+  double* reward;
+  void* inv;
+  void* bl;
+  void* ou;
+  void* ring;
+  int32_t* carry;
+  int32_t* bto;
+  void* hist_d;
+  void* hist_o;
+  const int32_t* demand;      // PER_ENV: [T][R][n]; BROADCAST: [T][R]
+  const double* delay_u;      // [T][N][n] or null
+  uint32_t* err;              // [n]
+  uint32_t* err_any;          // [1]
+  int32_t* i_order;
+  int32_t* i_demand;
+  int32_t* i_acq;
+  int32_t* i_ship;
+  double* i_profit;
+  int32_t* i_ship_to;
+  int32_t* i_bto;
+  const float* lut32;
+  const double* lut64;
+  const uint32_t* episode;    // device word written by the reset kernel (graph-replay safe)
+  int64_t n;
+  uint32_t env_offset;
+  int32_t t;
+  int32_t action_f64;
+  int32_t obs_f64;
+  int32_t demand_layout;      // IMENV_LAYOUT_*
+  int32_t noisy_demand;       // applies to drawn / broadcast demand
+  int32_t noisy_delay;
+  int32_t arr_row;            // t mod D
+  double noisy_delay_thr;
+  uint64_t noisy_delay_thr32;
+  uint64_t noisy_demand_thr32;
+  int32_t dep_row[IMENV_MAX_NODES];   // (t + delay[i]) mod D
+};
+
+constexpr uint32_t PH_M0 = 0xD2511F53u, PH_M1 = 0xCD9E8D57u;
+constexpr uint32_t PH_W0 = 0x9E3779B9u, PH_W1 = 0xBB67AE85u;
+constexpr uint32_t STREAM_DEMAND = 0, STREAM_ND_DOUBLE = 1, STREAM_ND_ZERO = 2, STREAM_NOISY_DELAY = 3;
+
+// Philox4x32-10 (Salmon et al. SC'11); oracle/philox.py is the CPU twin.
+__device__ __forceinline__ uint32_t philox_word(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                                uint32_t k0, uint32_t k1, int w) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += PH_W0; k1 += PH_W1; }
+    const uint32_t hi0 = __umulhi(PH_M0, c0), lo0 = PH_M0 * c0;
+    const uint32_t hi1 = __umulhi(PH_M1, c2), lo1 = PH_M1 * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+  }
+  return w == 0 ? c0 : (w == 1 ? c1 : (w == 2 ? c2 : c3));
+}
+
+__device__ __forceinline__ int ceil_div_pos(int a, int b) { return (a + b - 1) / b; }
+
+// Round-robin unit shipping, closed form. Restates the reference's
+//   while <cond> and amt > 0: for k in children: if x[k] > 0: s[k]+=1; x[k]-=1; amt-=1
+// (IM_div_env.py:413-428, 440-450, 472-484; the inner loop does not re-check amt).
+// SUMCHECK: loop also requires sum(x) > 0 (backlog-first / outstanding-order loops).
+// Without it (capped loop, IM_div_env.py:488-498) an env with nothing eligible spins
+// until the guard trips. Phases: while the set P = {k: x[k] > 0} is fixed, every
+// round moves |P| units, so a phase lasts min(min_P x, ceil(S/|P|), ceil(amt/|P|))
+// rounds. Returns false if the guard (rounds > lim) trips; rounds stop at lim+1.
+template <int MC, bool SUMCHECK>
+__device__ __forceinline__ bool rr_closed(int m, int (&x)[MC], int (&s)[MC], int& amt, int lim) {
+  int rounds = 0;
+#pragma unroll 1
+  for (int ph = 0; ph <= MC + 1; ++ph) {
+    int S = 0, cnt = 0, mn = INT_MAX;
+#pragma unroll
+    for (int k = 0; k < MC; ++k) {
+      if (k < m) {
+        S += x[k];
+        if (x[k] > 0) { ++cnt; mn = min(mn, x[k]); }
+      }
+    }
+    if (amt <= 0) break;
+    if (SUMCHECK && S <= 0) break;
+    if (cnt == 0) { rounds = lim + 1; break; }   // no progress possible: guard trips
+    int r = min(mn, ceil_div_pos(amt, cnt));
+    if (SUMCHECK) r = min(r, ceil_div_pos(S, cnt));
+    const int rem = lim + 1 - rounds;
+    if (r > rem) r = rem;
+#pragma unroll
+    for (int k = 0; k < MC; ++k)
+      if (k < m && x[k] > 0) { x[k] -= r; s[k] += r; }
+    amt -= r * cnt;
+    rounds += r;
+    if (rounds > lim) break;
+  }
+  return rounds <= lim;
+}
+
+template <int NT>
+__device__ __forceinline__ int sel(const int (&v)[NT], int idx) {
+  int r = 0;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) r = (idx == j) ? v[j] : r;
+  return r;
+}
+
+__device__ __forceinline__ double obs_map(int mode, double v, double a, double bma, double den, double clip) {
+  // rescale(val, 0, max, a, b) = a + ((val - 0) * (b - a)) / (max - 0)   (IM_env.py:435-444)
+  if (mode == IMENV_OBS_RAW) return v;
+  if (mode == IMENV_OBS_SCALED) return a + (v * bma) / den;
+  if (mode == IMENV_OBS_CLAMP_SCALED) return a + (fmin(v, clip) * bma) / den;
+  return 0.0;
+}
+
+// ---------------------------------------------------------------- raw loads
+// Loads move bytes into raw 32-bit words and nothing else: all unpacking happens after every load
+// of the step has been issued, so hipcc places a single vmcnt wait at the first use instead of one
+// wait per load (a wave's loads then overlap instead of paying HBM latency one after another).
+template <int BYTES>
+__device__ __forceinline__ void load_words(const void* __restrict__ p, uint32_t (&w)[BYTES / 4]) {
+  constexpr int W = BYTES / 4;
+  if constexpr (BYTES % 16 == 0) {
+#pragma unroll
+    for (int q = 0; q < W / 4; ++q) {
+      const uint4 x = reinterpret_cast<const uint4*>(p)[q];
+      w[4 * q] = x.x; w[4 * q + 1] = x.y; w[4 * q + 2] = x.z; w[4 * q + 3] = x.w;
+    }
+  } else if constexpr (BYTES % 8 == 0) {
+#pragma unroll
+    for (int q = 0; q < W / 2; ++q) {
+      const uint2 x = reinterpret_cast<const uint2*>(p)[q];
+      w[2 * q] = x.x; w[2 * q + 1] = x.y;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < W; ++q) w[q] = reinterpret_cast<const uint32_t*>(p)[q];
+  }
+}
+
+template <int BYTES>
+__device__ __forceinline__ void store_words(void* __restrict__ p, const uint32_t (&w)[BYTES / 4]) {
+  constexpr int W = BYTES / 4;
+  if constexpr (BYTES % 16 == 0) {
+#pragma unroll
+    for (int q = 0; q < W / 4; ++q)
+      reinterpret_cast<uint4*>(p)[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  } else if constexpr (BYTES % 8 == 0) {
+#pragma unroll
+    for (int q = 0; q < W / 2; ++q) reinterpret_cast<uint2*>(p)[q] = make_uint2(w[2 * q], w[2 * q + 1]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < W; ++q) reinterpret_cast<uint32_t*>(p)[q] = w[q];
+  }
+}
+
+// A packed row is NP elements of ST at base + e*NP. EXACT rows (N == NT) move as whole
+// 4/8/16-byte words (one vector instruction per lane); padded rows element-wise. Both forms
+// deliver raw words; unpack() turns them into ints.
+template <typename ST, int NT, bool EXACT>
+struct Row {
+  static constexpr int NPT = (sizeof(ST) == 2) ? ((NT + 1) & ~1) : NT;
+  static constexpr int BYTES = NPT * (int)sizeof(ST);
+  static constexpr int WORDS = BYTES / 4;
+
+  __device__ static __forceinline__ void load(const ST* __restrict__ base, int64_t e, int np, int N,
+                                              uint32_t (&w)[WORDS]) {
+    if (EXACT || np == NPT) {
+      load_words<BYTES>(base + e * NPT, w);
+    } else {
+#pragma unroll
+      for (int q = 0; q < WORDS; ++q) w[q] = 0;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        if (i < N) {
+          if constexpr (sizeof(ST) == 2) w[i >> 1] |= ((uint32_t)(uint16_t)base[e * np + i]) << ((i & 1) * 16);
+          else w[i] = (uint32_t)base[e * np + i];
+        }
+      }
+    }
+  }
+
+  __device__ static __forceinline__ void unpack(const uint32_t (&w)[WORDS], int (&v)[NT]) {
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      if constexpr (sizeof(ST) == 2) v[i] = (int)(int16_t)((w[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu);
+      else v[i] = (int)w[i];
+    }
+  }
+
+  __device__ static __forceinline__ void load_unpacked(const ST* __restrict__ base, int64_t e, int np, int N,
+                                                       int (&v)[NT]) {
+    uint32_t w[WORDS];
+    load(base, e, np, N, w);
+    unpack(w, v);
+  }
+
+  __device__ static __forceinline__ void store(ST* __restrict__ base, int64_t e, int np, int N, const int (&v)[NT]) {
+    if (EXACT || np == NPT) {
+      uint32_t w[WORDS];
+#pragma unroll
+      for (int q = 0; q < WORDS; ++q) w[q] = 0;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const int x = (i < N) ? v[i] : 0;
+        if constexpr (sizeof(ST) == 2) w[i >> 1] |= ((uint32_t)(uint16_t)(int16_t)x) << ((i & 1) * 16);
+        else w[i] = (uint32_t)x;
+      }
+      store_words<BYTES>(base + e * NPT, w);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) if (i < N) base[e * np + i] = (ST)v[i];
+    }
+  }
+};
+
+// ---------------------------------------------------------------- runtime spec policy
+// Every accessor reads the spec from device memory (scalar loads). Per-call flags come from A.
+template <int NT_, int MC_, bool BASE_, typename ST_>
+struct DynSpec {
+  static constexpr int NT = NT_;
+  static constexpr int MC = MC_;
+  static constexpr bool BASE = BASE_;
+  static constexpr bool EXACT = NT_ <= 8;    // AOT kernels for N <= 8 are compiled for N == NT
+  static constexpr bool JIT = false;
+  using ST = ST_;
+  const SpecDev* __restrict__ sp;
+  const StepArgs& A;
+  __device__ DynSpec(const SpecDev* __restrict__ s, const StepArgs& a) : sp(s), A(a) {}
+  __device__ int N() const { return EXACT ? NT : sp->s.num_nodes; }
+  __device__ int T() const { return sp->s.num_periods; }
+  __device__ int np() const { return EXACT ? Row<ST, NT, EXACT>::NPT : sp->np; }
+  __device__ int D() const { return sp->dmax; }
+  __device__ int factory() const { return sp->factory; }
+  __device__ int num_retailers() const { return sp->s.num_retailers; }
+  __device__ int prev_length() const { return sp->s.prev_length; }
+  __device__ int num_features() const { return sp->s.num_features; }
+  __device__ int num_split() const { return sp->num_split; }
+  __device__ int delay(int i) const { return sp->s.delay[i]; }
+  __device__ int init_inv(int i) const { return sp->s.init_inv[i]; }
+  __device__ int inv_max(int i) const { return sp->s.inv_max[i]; }
+  __device__ int order_max(int i) const { return sp->s.order_max[i]; }
+  __device__ int backlog_cap(int i) const { return sp->s.backlog_cap[i]; }
+  __device__ int retailer_slot(int i) const { return sp->s.retailer_slot[i]; }
+  __device__ int demand_parent(int c) const { return sp->s.demand_parent[c]; }
+  __device__ int single_parent(int c) const { return sp->single_parent[c]; }
+  __device__ int split_child(int c) const { return sp->split_child[c]; }
+  __device__ int split_node(int si) const { return sp->split_node[si]; }
+  __device__ int num_children(int p) const { return sp->s.num_children[p]; }
+  __device__ int child(int p, int k) const { return sp->s.children[p][k]; }
+  __device__ int split_limit(int p, int q) const { return sp->s.split_limit[p][q]; }
+  __device__ double sell(int i) const { return sp->s.sell_price[i]; }
+  __device__ double buy(int i) const { return sp->s.buy_price[i]; }
+  __device__ double stock_cost(int i) const { return sp->s.stock_cost[i]; }
+  __device__ double backlog_cost(int i) const { return sp->s.backlog_cost[i]; }
+  __device__ double inv_target(int i) const { return sp->s.inv_target[i]; }
+  __device__ bool std_actions() const { return sp->s.standardise_actions != 0; }
+  __device__ bool clip_round() const { return sp->s.decode_mode == IMENV_DECODE_CLIP_ROUND; }
+  __device__ double a() const { return sp->s.a; }
+  __device__ double bma() const { return sp->s.b - sp->s.a; }
+  __device__ double inv_bma() const { return sp->inv_bma; }
+  __device__ int reward_mode() const { return sp->s.reward_mode; }
+  __device__ double inv_n() const { return sp->inv_n; }
+  __device__ int group_mode(int g) const { return sp->s.group_mode[g]; }
+  __device__ double group_den(int g, int i) const { return sp->s.group_den[g][i]; }
+  __device__ double group_clip(int g, int i) const { return sp->s.group_clip[g][i]; }
+  __device__ int lut_max(int g, int i) const { return sp->lut_max[g][i]; }
+  __device__ int lut_off(int g, int i) const { return sp->lut_off[g][i]; }
+  __device__ int feat_group(int f) const { return sp->s.feat_group[f]; }
+  __device__ int feat_index(int f) const { return sp->s.feat_index[f]; }
+  __device__ int demand_dist() const { return sp->s.demand_dist; }
+  __device__ int uniform_low() const { return sp->s.uniform_low; }
+  __device__ int uniform_high() const { return sp->s.uniform_high; }
+  __device__ uint64_t seed() const { return sp->s.seed; }
+  // per-call flags
+  __device__ bool act_f64() const { return A.action_f64 != 0; }
+  __device__ int demand_layout() const { return A.demand_layout; }
+  __device__ bool noisy_delay() const { return A.noisy_delay != 0; }
+  __device__ bool noisy_demand() const { return A.noisy_demand != 0; }
+  __device__ bool has_delay_u() const { return A.delay_u != nullptr; }
+  __device__ bool uses_hist() const { return A.hist_d != nullptr; }
+  // Poisson inversion: binary search over the LDS copy of the table
+  __device__ int poisson_draw(uint32_t w, const uint32_t* s_tab) const {
+    int lo = 0, hi = sp->table_len;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (w >= s_tab[mid]) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+  }
+  __device__ void stage_tables(uint32_t* s_tab, bool poisson) const {
+    if (poisson) {
+      for (int k = threadIdx.x; k < sp->table_len; k += 256) s_tab[k] = sp->table[k];
+      __syncthreads();
+    }
+  }
+};
+
+// Exact observation value for integer raw value v: table lookup (host-built with the same IEEE
+// double expression, so bit-identical) inside the tabulated range, else computed.
+template <class P>
+__device__ __forceinline__ double obs_value64(const P& p, const double* __restrict__ lut, int g, int i, int v) {
+  const int mx = p.lut_max(g, i);
+  if (v >= 0 && v <= mx) return lut[p.lut_off(g, i) + v];
+  return obs_map(p.group_mode(g), (double)v, p.a(), p.bma(), p.group_den(g, i), p.group_clip(g, i));
+}
+template <class P>
+__device__ __forceinline__ float obs_value32(const P& p, const float* __restrict__ lut, int g, int i, int v) {
+  const int mx = p.lut_max(g, i);
+  if (v >= 0 && v <= mx) return lut[p.lut_off(g, i) + v];
+  return (float)obs_map(p.group_mode(g), (double)v, p.a(), p.bma(), p.group_den(g, i), p.group_clip(g, i));
+}
+
+// ---------------------------------------------------------------- step body
+// Structure: (A) issue every load that does not depend on this step's arithmetic (raw words),
+// (B) compute in registers, (C) store; float32 BASE observations are staged through LDS so the
+// block writes its contiguous obs slab with full 1 KiB-per-wave float4 stores.
+template <class P>
+__device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_t* s_tab, float* s_obs) {
+  constexpr int NT = P::NT;
+  constexpr int MC = P::MC;
+  constexpr bool EXACT = P::EXACT;
+  constexpr bool STAGE = P::BASE && NT <= 8;
+  using ST = typename P::ST;
+  using R = Row<ST, NT, EXACT>;
+  using R32 = Row<int32_t, NT, EXACT>;
+  const int tid = threadIdx.x;
+  const int64_t e0 = (int64_t)blockIdx.x * 256;
+  const int64_t e = e0 + tid;
+  const int64_t n = A.n;
+  const bool valid = e < n;
+  const int N = p.N();
+  const int T = p.T();
+  const int np = p.np();
+  const int t = A.t;
+  const bool poisson = p.demand_layout() == IMENV_LAYOUT_DRAW && p.demand_dist() == IMENV_DEMAND_POISSON;
+
+  ST* __restrict__ p_inv = static_cast<ST*>(A.inv);
+  ST* __restrict__ p_bl = static_cast<ST*>(A.bl);
+  ST* __restrict__ p_ou = static_cast<ST*>(A.ou);
+  ST* __restrict__ p_ring = static_cast<ST*>(A.ring);
+  int32_t* __restrict__ p_carry = A.carry;
+  int32_t* __restrict__ p_bto = A.bto;
+  const int64_t ring_rows = n * np;   // elements per ring row
+
+  // ================= (A) loads: raw words only, every independent load issued before any use
+  uint32_t aw[2 * NT];
+  uint32_t w_inv[R::WORDS], w_bl[R::WORDS], w_ou[R::WORDS], w_arr[R::WORDS], w_cin[R32::WORDS], w_bto[R32::WORDS];
+  int cdem[NT];
+  double du[NT];
+#pragma unroll
+  for (int q = 0; q < 2 * NT; ++q) aw[q] = 0;
+#pragma unroll
+  for (int q = 0; q < R::WORDS; ++q) w_inv[q] = w_bl[q] = w_ou[q] = w_arr[q] = 0;
+#pragma unroll
+  for (int q = 0; q < R32::WORDS; ++q) w_cin[q] = w_bto[q] = 0;
+#pragma unroll
+  for (int i = 0; i < NT; ++i) { cdem[i] = 0; du[i] = 1.0; }
+  if (valid) {
+    if (EXACT) {
+      if (p.act_f64()) {
+        load_words<8 * NT>(static_cast<const double*>(A.actions) + e * NT, aw);
+      } else {
+        uint32_t (&a32)[NT] = *reinterpret_cast<uint32_t(*)[NT]>(aw);
+        load_words<4 * NT>(static_cast<const float*>(A.actions) + e * NT, a32);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        if (i < N) {
+          if (p.act_f64()) {
+            const uint2 v = reinterpret_cast<const uint2*>(static_cast<const double*>(A.actions) + e * N)[i];
+            aw[2 * i] = v.x; aw[2 * i + 1] = v.y;
+          } else {
+            aw[i] = reinterpret_cast<const uint32_t*>(static_cast<const float*>(A.actions) + e * N)[i];
+          }
+        }
+      }
+    }
+    // state and arrivals are loaded even at t == 0 (then ignored): unconditional, branch-free loads
+    R::load(p_inv, e, np, N, w_inv);
+    R::load(p_bl, e, np, N, w_bl);
+    R::load(p_ou, e, np, N, w_ou);
+    R::load(p_ring + (int64_t)A.arr_row * ring_rows, e, np, N, w_arr);
+    if (p.noisy_delay()) R32::load(p_carry, e, np, N, w_cin);
+    if (MC > 0) R32::load(p_bto, e, np, N, w_bto);
+    if (p.demand_layout() == IMENV_LAYOUT_PER_ENV) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const int r = (i < N) ? p.retailer_slot(i) : -1;
+        if (r >= 0) cdem[i] = A.demand[((int64_t)t * p.num_retailers() + r) * n + e];
+      }
+    }
+    if (p.has_delay_u()) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) if (i < N) du[i] = A.delay_u[((int64_t)t * N + i) * n + e];
+    }
+  }
+  p.stage_tables(s_tab, poisson);
+
+  // unpack (first use of the loaded words)
+  double x[NT];
+  int inv[NT], bl[NT], ou[NT], arr[NT], cin[NT], btoc[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    if (p.act_f64()) x[i] = __hiloint2double((int)aw[2 * i + 1], (int)aw[2 * i]);
+    else x[i] = (double)__uint_as_float(aw[i]);
+  }
+  R::unpack(w_inv, inv);
+  R::unpack(w_bl, bl);
+  R::unpack(w_ou, ou);
+  R::unpack(w_arr, arr);
+  R32::unpack(w_cin, cin);
+  R32::unpack(w_bto, btoc);
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    if (t == 0) {            // period-0 state is implicit (IM_env.py:221-224)
+      inv[i] = (i < N) ? p.init_inv(i) : 0;
+      bl[i] = ou[i] = cin[i] = btoc[i] = 0;
+    }
+    if (i >= N || t < p.delay(i < N ? i : 0)) arr[i] = 0;   // nothing shipped d periods ago yet
+  }
+
+  // ================= (B) compute
+  const uint32_t ep = *A.episode;
+  const uint32_t gid = A.env_offset + (uint32_t)e;
+  const uint64_t seed = p.seed();
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const double a = p.a();
+  const double bma = p.bma();
+  int order[NT], dem[NT], acq[NT], ship[NT], sto[NT], cout[NT], push[NT];
+  double prof[NT];
+  // order decode (IM_env.py:298-302; MAIM_env.py:340-347). Division by b - a is replaced by
+  // an exact multiply when b - a is a power of two (inv_bma != 0).
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    order[i] = 0;
+    if (i < N) {
+      const double om = (double)p.order_max(i);
+      double v = x[i];
+      if (p.std_actions()) {
+        const double q = (x[i] - a) * (om - 0.0);
+        v = (p.inv_bma() != 0.0 ? q * p.inv_bma() : q / bma) + 0.0;
+      }
+      const double o = p.clip_round() ? rint(fmin(fmax(v, 0.0), om)) : fmin(fmax(rint(v), 0.0), om);
+      order[i] = (int)o;
+    }
+  }
+  // demand (IM_env.py:306-308, IM_div_env.py:380-387)
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    dem[i] = 0;
+    if (i < N) {
+      const int r = p.retailer_slot(i);
+      if (r >= 0) {
+        int cd;
+        if (p.demand_layout() == IMENV_LAYOUT_PER_ENV) {
+          cd = cdem[i];
+        } else if (p.demand_layout() == IMENV_LAYOUT_BROADCAST) {
+          cd = A.demand[t * p.num_retailers() + r];
+        } else {
+          const uint32_t w = philox_word(gid, ep, (uint32_t)t, (STREAM_DEMAND << 16) | (uint32_t)(r >> 2), k0, k1,
+                                         r & 3);
+          if (poisson) {
+            cd = p.poisson_draw(w, s_tab);
+          } else {
+            const uint64_t rng = (uint64_t)(p.uniform_high() - p.uniform_low());
+            cd = p.uniform_low() + (int)(((uint64_t)w * rng) >> 32);
+          }
+        }
+        if (p.noisy_demand()) {
+          const uint32_t wd = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_DOUBLE << 16) | (uint32_t)(r >> 2), k0, k1,
+                                          r & 3);
+          const uint32_t wz = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_ZERO << 16) | (uint32_t)(r >> 2), k0, k1,
+                                          r & 3);
+          if ((uint64_t)wd < A.noisy_demand_thr32) cd = 2 * cd;
+          if ((uint64_t)wz < A.noisy_demand_thr32) cd = 0;
+        }
+        dem[i] = min(cd, p.inv_max(i));
+      } else {
+        int s = 0;
+#pragma unroll
+        for (int c = 0; c < NT; ++c)
+          if (c < N && p.demand_parent(c) == i) s += order[c];
+        dem[i] = s;
+      }
+    }
+  }
+  // arrivals (IM_env.py:376-414); noisy delay defers the whole arrival (plus any carried amount)
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    acq[i] = ship[i] = cout[i] = 0;
+    if (i < N) {
+      int q = arr[i] + cin[i];
+      if (p.noisy_delay() && t >= p.delay(i)) {
+        bool extra;
+        if (p.has_delay_u()) extra = du[i] <= A.noisy_delay_thr;
+        else extra = (uint64_t)philox_word(gid, ep, (uint32_t)t, (STREAM_NOISY_DELAY << 16) | (uint32_t)(i >> 2),
+                                           k0, k1, i & 3) < A.noisy_delay_thr32;
+        if (extra && t < T - 1) { cout[i] = q; q = 0; }
+      }
+      acq[i] = q;
+      ship[i] = min(bl[i] + dem[i], inv[i] + acq[i]);   // IM_env.py:315
+    }
+  }
+  // shipments into each node: a single-child parent's whole shipment, else the split
+#pragma unroll
+  for (int c = 0; c < NT; ++c) {
+    sto[c] = 0;
+    if (c < N) {
+      const int par = p.single_parent(c);
+      if (par >= 0) sto[c] = sel<NT>(ship, par);
+    }
+  }
+  bool split_ok = true;
+  if constexpr (MC > 0) {
+#pragma unroll
+    for (int si = 0; si < NT; ++si) {
+      if (si >= p.num_split()) break;
+      const int q = p.split_node(si);
+      const int m = p.num_children(q);
+      const int shp = sel<NT>(ship, q), dmp = sel<NT>(dem, q), blp = sel<NT>(bl, q);
+      int bto[MC], oc[MC], s[MC];
+#pragma unroll
+      for (int k = 0; k < MC; ++k) {
+        s[k] = 0; bto[k] = 0; oc[k] = 0;
+        if (k < m) {
+          const int c = p.child(q, k);
+          oc[k] = sel<NT>(order, c);
+          bto[k] = sel<NT>(btoc, c);
+        }
+      }
+      int amt = shp;
+      bool ok = true;
+      if (shp >= dmp) {
+        if (blp > 0) {        // backlog first, then outstanding orders (IM_div_env.py:409-454)
+          ok = rr_closed<MC, true>(m, bto, s, amt, p.split_limit(q, 0));
+          if (ok && amt > 0 && dmp > 0) {
+            int out[MC];
+#pragma unroll
+            for (int k = 0; k < MC; ++k) out[k] = oc[k];
+            ok = rr_closed<MC, true>(m, out, s, amt, p.split_limit(q, 1));
+#pragma unroll
+            for (int k = 0; k < MC; ++k) bto[k] += out[k];
+          }
+        } else {              // IM_div_env.py:457-460
+#pragma unroll
+          for (int k = 0; k < MC; ++k) s[k] += oc[k];
+        }
+      } else {
+        if (blp > 0) {        // IM_div_env.py:468-484
+          ok = rr_closed<MC, true>(m, bto, s, amt, p.split_limit(q, 2));
+        } else {              // IM_div_env.py:486-498: cap at order + backlog_to
+          int cap[MC];
+#pragma unroll
+          for (int k = 0; k < MC; ++k) cap[k] = oc[k] + bto[k];
+          ok = rr_closed<MC, false>(m, cap, s, amt, p.split_limit(q, 3));
+        }
+#pragma unroll
+        for (int k = 0; k < MC; ++k) bto[k] += oc[k] - s[k];   // IM_div_env.py:501-502
+      }
+      split_ok = split_ok && ok;
+#pragma unroll
+      for (int k = 0; k < MC; ++k) {
+        if (k < m) {
+          const int c = p.child(q, k);
+#pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            sto[j] = (c == j) ? s[k] : sto[j];
+            btoc[j] = (c == j) ? bto[k] : btoc[j];
+          }
+        }
+      }
+    }
+  }
+  // balance equations and profit (IM_env.py:318-340, 362-367)
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    prof[i] = 0.0;
+    push[i] = 0;
+    if (i < N) {
+      int b2 = bl[i] + dem[i] - ship[i];
+      if (p.backlog_cap(i) >= 0) b2 = min(b2, p.backlog_cap(i));
+      const int im = p.inv_max(i);
+      const int ou2 = min(max(ou[i] + order[i] - acq[i], 0), im);
+      const int inv2 = min(max(inv[i] + acq[i] - ship[i], 0), im);
+      prof[i] = ((p.sell(i) * (double)ship[i] - p.buy(i) * (double)order[i]) -
+                 p.stock_cost(i) * fabs((double)inv2 - p.inv_target(i))) -
+                p.backlog_cost(i) * (double)b2;
+      bl[i] = b2; ou[i] = ou2; inv[i] = inv2;
+      push[i] = (i == p.factory()) ? order[i] : sto[i];
+    }
+  }
+  // reward (IM_env.py:372 np.sum order; MAIM_env.py:418-434)
+  double rew = 0.0;
+  if (p.reward_mode() != IMENV_REWARD_INDEPENDENT) {
+    if (p.reward_mode() == IMENV_REWARD_SHARED_MEAN || N < 8) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) if (i < N) rew += prof[i];
+      if (p.reward_mode() == IMENV_REWARD_SHARED_MEAN) rew = (p.inv_n() != 0.0) ? rew * p.inv_n() : rew / (double)N;
+    } else {
+      double r8[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r8[j] = (j < NT) ? prof[j < NT ? j : 0] : 0.0;
+      const int full = N - (N % 8);
+#pragma unroll
+      for (int i0 = 8; i0 < NT; i0 += 8) {
+        if (i0 < full) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) if (i0 + j < NT) r8[j] += prof[(i0 + j) < NT ? i0 + j : 0];
+        }
+      }
+      rew = ((r8[0] + r8[1]) + (r8[2] + r8[3])) + ((r8[4] + r8[5]) + (r8[6] + r8[7]));
+#pragma unroll
+      for (int i = 8; i < NT; ++i) if (i >= full && i < N) rew += prof[i];
+    }
+  }
+
+  // ================= (C) stores
+  if (valid) {
+    R::store(p_inv, e, np, N, inv);
+    R::store(p_bl, e, np, N, bl);
+    R::store(p_ou, e, np, N, ou);
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+      if (i < N) p_ring[(int64_t)A.dep_row[i] * ring_rows + e * np + i] = (ST)push[i];
+    if (p.noisy_delay()) R32::store(p_carry, e, np, N, cout);
+    if (MC > 0) R32::store(p_bto, e, np, N, btoc);
+    if (!split_ok) {          // no-return atomics
+      atomicOr(A.err + e, 1u);
+      atomicOr(A.err_any, 1u);
+    }
+    if (p.uses_hist()) {
+      const int L = p.prev_length();
+      R::store(static_cast<ST*>(A.hist_d) + (int64_t)(t % L) * ring_rows, e, np, N, dem);
+      R::store(static_cast<ST*>(A.hist_o) + (int64_t)(t % L) * ring_rows, e, np, N, order);
+    }
+    if (p.reward_mode() == IMENV_REWARD_INDEPENDENT) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) if (i < N) A.reward[e * N + i] = prof[i];
+    } else {
+      A.reward[e] = rew;
+    }
+    if (A.i_order) {   // info (IM_env.py:345-350)
+#pragma unroll
+      for (int i = 0; i < NT; ++i) if (i < N) {
+        A.i_order[e * N + i] = order[i];
+        if (A.i_demand) A.i_demand[e * N + i] = dem[i];
+        if (A.i_acq) A.i_acq[e * N + i] = acq[i];
+        if (A.i_ship) A.i_ship[e * N + i] = ship[i];
+        if (A.i_profit) A.i_profit[e * N + i] = prof[i];
+        if (A.i_ship_to) A.i_ship_to[e * N + i] = sto[i];
+        if (A.i_bto) A.i_bto[e * N + i] = p.split_child(i) ? btoc[i] : 0;
+      }
+    }
+  }
+
+  // observation for period t+1 (IM_env.py:231-285, MAIM_env.py:242-328, IM_div_env.py:304-359,
+  // MAIM_div_env.py:343-439)
+  if constexpr (P::BASE) {
+    if (STAGE && !A.obs_f64) {
+      const int row = 3 * N;
+      if (valid) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+          if (i < N) {
+            s_obs[tid * row + 3 * i + 0] = obs_value32(p, A.lut32, IMENV_G_INV, i, inv[i]);
+            s_obs[tid * row + 3 * i + 1] = obs_value32(p, A.lut32, IMENV_G_BACKLOG, i, bl[i]);
+            s_obs[tid * row + 3 * i + 2] = obs_value32(p, A.lut32, IMENV_G_ORDER_U, i, ou[i]);
+          }
+        }
+      }
+      __syncthreads();
+      const int64_t cnt = (n - e0) < 256 ? (n - e0) : 256;
+      const int64_t total = cnt * row;
+      float* gobs = static_cast<float*>(A.obs) + e0 * row;
+      if ((total & 3) == 0) {
+        float4* g4 = reinterpret_cast<float4*>(gobs);
+        const float4* s4 = reinterpret_cast<const float4*>(s_obs);
+        for (int64_t q = tid; q < total / 4; q += 256) g4[q] = s4[q];
+      } else {
+        for (int64_t q = tid; q < total; q += 256) gobs[q] = s_obs[q];
+      }
+    } else if (valid) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        if (i < N) {
+          const int64_t base = (e * N + i) * 3;
+          if (A.obs_f64) {
+            double* o = static_cast<double*>(A.obs);
+            o[base + 0] = obs_value64(p, A.lut64, IMENV_G_INV, i, inv[i]);
+            o[base + 1] = obs_value64(p, A.lut64, IMENV_G_BACKLOG, i, bl[i]);
+            o[base + 2] = obs_value64(p, A.lut64, IMENV_G_ORDER_U, i, ou[i]);
+          } else {
+            float* o = static_cast<float*>(A.obs);
+            o[base + 0] = obs_value32(p, A.lut32, IMENV_G_INV, i, inv[i]);
+            o[base + 1] = obs_value32(p, A.lut32, IMENV_G_BACKLOG, i, bl[i]);
+            o[base + 2] = obs_value32(p, A.lut32, IMENV_G_ORDER_U, i, ou[i]);
+          }
+        }
+      }
+    }
+  } else if (valid) {
+    const int F = p.num_features();
+    const int L = p.prev_length();
+    const int D = p.D();
+    const int tp = t + 1;   // observation period
+#pragma unroll 1
+    for (int f = 0; f < F; ++f) {
+      const int g = p.feat_group(f);
+      const int j = p.feat_index(f);
+      int v[NT];
+#pragma unroll
+      for (int i = 0; i < NT; ++i) v[i] = 0;
+      if (g == IMENV_G_INV) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) v[i] = inv[i];
+      } else if (g == IMENV_G_BACKLOG) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) v[i] = bl[i];
+      } else if (g == IMENV_G_ORDER_U) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) v[i] = ou[i];
+      } else if (g == IMENV_G_DEMAND_HIST || g == IMENV_G_ORDER_HIST) {
+        const int pr = tp - 1 - j;     // period of the entry; 0 when j >= tp
+        if (pr >= 0) {
+          if (j == 0) {
+#pragma unroll
+            for (int i = 0; i < NT; ++i) v[i] = (g == IMENV_G_DEMAND_HIST) ? dem[i] : order[i];
+          } else {
+            const ST* h = static_cast<const ST*>(g == IMENV_G_DEMAND_HIST ? A.hist_d : A.hist_o);
+            R::load_unpacked(h + (int64_t)(pr % L) * ring_rows, e, np, N, v);
+          }
+        }
+      } else if (g == IMENV_G_TRANSIT) {
+        // slot j: amount arriving at period tp + j, i.e. ring row (t + 1 + j) mod D, written at
+        // tp + j - d_i (IM_env.py:416-432); the slot d_i - 1 was written by this step
+        int rv[NT];
+        R::load_unpacked(p_ring + (int64_t)((A.arr_row + 1 + j) % D) * ring_rows, e, np, N, rv);
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+          const int d = (i < N) ? p.delay(i) : 1;
+          v[i] = 0;
+          if (i < N && j < d && tp + j - d >= 0) v[i] = (j == d - 1) ? push[i] : rv[i];
+        }
+      } else if (g == IMENV_G_NODE_ID) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) v[i] = i;
+      }
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        if (i < N) {
+          const int64_t idx = (e * N + i) * F + f;
+          if (A.obs_f64) static_cast<double*>(A.obs)[idx] = obs_value64(p, A.lut64, g, i, v[i]);
+          else static_cast<float*>(A.obs)[idx] = obs_value32(p, A.lut32, g, i, v[i]);
+        }
+      }
+    }
+  }
+}
+
+// obs staging buffer size (floats) for a policy
+template <class P>
+constexpr int stage_floats() {
+  return (P::BASE && P::NT <= 8) ? 256 * 3 * P::NT : 4;
+}
+
+// Kernel template for any policy whose constructor takes (spec, args).
+template <class P>
+__global__ void __launch_bounds__(256) imenv_step_kernel(const SpecDev* __restrict__ sp, const StepArgs A) {
+  __shared__ uint32_t s_tab[P::JIT ? 1 : IMENV_TABLE_MAX];
+  __shared__ __attribute__((aligned(16))) float s_obs[stage_floats<P>()];
+  const P p(sp, A);
+  step_body(p, A, s_tab, s_obs);
+}
+
+#ifndef __HIPCC_RTC__
+struct LaunchCfg {
+  int mc;          // 0, 4, 8
+  bool base;
+  bool st16;
+  unsigned grid;   // number of 256-env blocks
+  hipStream_t stream;
+};
+
+template <int NT>
+void launch_step_nt(const LaunchCfg& c, const SpecDev* sp, const StepArgs& A);
+#endif
+
+}  // namespace imenv

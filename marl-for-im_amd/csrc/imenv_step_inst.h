@@ -1,0 +1,34 @@
+// Instantiates the ahead-of-time step kernels (runtime spec policy DynSpec) for one node capacity
+// IMENV_NT, one translation unit per NT so the variants compile in parallel. Included by
+// imenv_step_nt{1..8,16}.hip: NT <= 8 kernels are exact (N == NT), NT = 16 serves 9..16 nodes with
+// runtime padding.
+#include "imenv_device.h"
+
+namespace imenv {
+namespace {
+template <int MC, bool BASE, typename ST>
+void go(const LaunchCfg& c, const SpecDev* sp, const StepArgs& A) {
+  hipLaunchKernelGGL((imenv_step_kernel<DynSpec<IMENV_NT, MC, BASE, ST>>), dim3(c.grid), dim3(256), 0, c.stream, sp,
+                     A);
+}
+template <int MC>
+void go_mc(const LaunchCfg& c, const SpecDev* sp, const StepArgs& A) {
+  if (c.base) {
+    if (c.st16) go<MC, true, int16_t>(c, sp, A); else go<MC, true, int32_t>(c, sp, A);
+  } else {
+    if (c.st16) go<MC, false, int16_t>(c, sp, A); else go<MC, false, int32_t>(c, sp, A);
+  }
+}
+}  // namespace
+
+template <>
+void launch_step_nt<IMENV_NT>(const LaunchCfg& c, const SpecDev* sp, const StepArgs& A) {
+  if constexpr (IMENV_NT >= 6) {
+    if (c.mc > 4) { go_mc<IMENV_MAX_CHILDREN>(c, sp, A); return; }
+  }
+  if constexpr (IMENV_NT >= 3) {
+    if (c.mc > 0) { go_mc<4>(c, sp, A); return; }
+  }
+  go_mc<0>(c, sp, A);
+}
+}  // namespace imenv

@@ -71,6 +71,7 @@ SYMBOLS = [
     ("imenv_get_errors", c_int, [c_void_p, c_void_p, POINTER(c_uint32), c_void_p]),
     ("imenv_dims", c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     ("imenv_poisson_table", c_int, [c_void_p, POINTER(c_uint32), c_int32, POINTER(c_int32)]),
+    ("imenv_state_layout", c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     ("imenv_destroy", None, [c_void_p]),
     ("imenv_last_error", ctypes.c_char_p, []),
     ("imenv_abi_version", c_int, []),

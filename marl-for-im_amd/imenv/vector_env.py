@@ -179,6 +179,12 @@ class VectorInvEnv:
         nat.check(self.lib.imenv_poisson_table(self._h, buf, ln.value, byref(ln)), "imenv_poisson_table")
         return np.array(buf[:ln.value], dtype=np.uint64)
 
+    def state_layout(self):
+        """(element bytes, row length, arrival-ring depth) of the packed HBM state."""
+        eb, rl, rd = c_int32(), c_int32(), c_int32()
+        nat.check(self.lib.imenv_state_layout(self._h, byref(eb), byref(rl), byref(rd)), "imenv_state_layout")
+        return eb.value, rl.value, rd.value
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             torch.cuda.synchronize(self.device)

@@ -1,0 +1,49 @@
+"""CPU checks of the drop-in boundary: libimenv.so loads (no GPU needed), exports every entry
+point include/imenv.h declares, and the ctypes ImEnvSpec layout matches the compiled one."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "imenv.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(imenv_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_the_abi():
+    names = declared_functions()
+    for must in ("imenv_create", "imenv_reset", "imenv_step", "imenv_get_state", "imenv_destroy",
+                 "imenv_last_error"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from imenv import _native
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libimenv.so not built (python __graft_entry__.py build)")
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    bound = {name for name, _, _ in _native.SYMBOLS}
+    assert bound == set(declared_functions()), set(declared_functions()) ^ bound
+
+
+def test_abi_version_and_spec_layout():
+    from imenv import _native
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libimenv.so not built")
+    lib = _native.load()
+    assert lib.imenv_abi_version() == _native.ABI_VERSION
+    assert lib.imenv_spec_size() == ctypes.sizeof(_native.ImEnvSpec)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    from imenv import _native
+    with pytest.raises(_native.ImEnvNativeError):
+        _native.load(str(tmp_path / "nope.so"))

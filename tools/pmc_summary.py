@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc CSVs: per-kernel mean counter values per dispatch.
+
+    python tools/pmc_summary.py OUT.json DIR [DIR ...]
+
+Each DIR is one rocprofv3 -d output (one --pmc pass). Kernel names are shortened
+to their template head. If the calibration kernels (tools/pmc_calib.hip, 1 GiB per
+dispatch) are present, FETCH_SIZE / WRITE_SIZE -> bytes factors are derived per
+access width and the step kernel's HBM traffic per launch is written to OUT.json.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+CAL_BYTES = float(1 << 30)
+
+
+def short(name):
+    m = re.search(r"(imenv_\w+?)(<[^>]*>)?\(", name)
+    if m:
+        return m.group(1) + (m.group(2) or "")
+    for k in ("read_dwordx4", "read_dword", "write_dwordx4", "write_dword"):
+        if re.search(r"\b%s\b" % k, name):
+            return k
+    return name[:60]
+
+
+def load(dirs):
+    acc = defaultdict(lambda: defaultdict(list))
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    k = short(row.get("Kernel_Name", ""))
+                    acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                    acc[k]["_grid"].append(float(row.get("Grid_Size", 0) or 0))
+    out = {}
+    for k, cs in acc.items():
+        out[k] = {c: (sum(v) / len(v)) for c, v in cs.items()}
+        out[k]["_dispatch_rows"] = len(cs.get("FETCH_SIZE", cs.get("WRITE_SIZE", [0])))
+    return out
+
+
+def main():
+    outp = sys.argv[1]
+    s = load(sys.argv[2:])
+    res = {"kernels": s}
+    fac = {}
+    for k, c in (("read_dword", "FETCH_SIZE"), ("read_dwordx4", "FETCH_SIZE"), ("write_dword", "WRITE_SIZE"),
+                 ("write_dwordx4", "WRITE_SIZE")):
+        if k in s and c in s[k] and s[k][c] > 0:
+            fac[k] = CAL_BYTES / (s[k][c] * 1024.0)
+    res["bytes_per_counter_kb_factor"] = fac
+    step = [k for k in s if k.startswith("imenv_step_kernel")]
+    if step and "read_dword" in fac and "write_dword" in fac:
+        k = step[0]
+        c = s[k]
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            rd = c["FETCH_SIZE"] * 1024.0 * fac["read_dword"]
+            wr = c["WRITE_SIZE"] * 1024.0 * fac["write_dword"]
+            res.update(kernel=k, hbm_read_bytes_per_launch=rd, hbm_write_bytes_per_launch=wr,
+                       hbm_bytes_per_launch=rd + wr,
+                       raw_fetch_kb=c["FETCH_SIZE"], raw_write_kb=c["WRITE_SIZE"])
+    with open(outp, "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+    print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
+    for k, c in s.items():
+        print(k, {a: round(b, 1) for a, b in c.items()})
+
+
+if __name__ == "__main__":
+    main()
