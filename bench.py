@@ -108,14 +108,14 @@ def _cpu_baseline_here(seconds):
 
 
 # ----------------------------------------------------------------- PMC traffic
-def pmc_traffic(n_envs):
+def pmc_traffic(n_envs, kernel):
     """HBM bytes per step-kernel launch from the committed rocprofv3 PMC summary
     (profiles/pmc_step_kernel.json, written by tools/pmc_summary.py for this workload), else None."""
     p = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if int(d.get("n_envs", -1)) == int(n_envs):
+        if int(d.get("n_envs", -1)) == int(n_envs) and d.get("kernel", "?") in kernel:
             return float(d["hbm_bytes_per_launch"])
     except Exception:
         pass
@@ -177,27 +177,27 @@ def main():
     o_ptr = [obs_buf[t].data_ptr() for t in range(T)]
     r_ptr = [rew_buf[t].data_ptr() for t in range(T)]
 
-    # HIP events bracket the step kernel on its own stream at two sampled periods per episode
-    # (t = 7, 22): a timing event pair costs ~7 us of GPU time, so timing every step would slow
-    # the very loop being measured (tools/launch_probe.py).
-    SAMPLE = (7, 22)
-
+    # HIP events on the kernel's own stream bracket the run of consecutive step launches t = 1..T-1 of
+    # every timed episode (no reset inside): per-launch duration = elapsed / (T - 1), back-to-back
+    # dispatch gaps included. One pair per episode: a pair per step would cost ~7 us of GPU time
+    # each and slow the very loop being measured (tools/launch_probe.py).
     def run(steps, events=None):
+        pair = None
         for s in range(steps):
             t = s % T
             if t == 0:
                 nat.check(lib.imenv_reset(h, None, nat.LAYOUT_DRAW, 0, 0.0, None, -1, obs0.data_ptr(), nat.F32,
                                           sptr), "imenv_reset")
-            ev = events is not None and t in SAMPLE
-            if ev:
+            if events is not None and t == 1 and s + T - 1 <= steps:
                 pair = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                events.append(pair)
                 pair[0].record(stream)
             rc = lib.imenv_step(h, a_ptr[t], nat.F32, o_ptr[t], nat.F32, r_ptr[t], None, None, sptr)
             if rc:
                 nat.check(rc, "imenv_step")
-            if ev:
+            if pair is not None and t == T - 1:
                 pair[1].record(stream)
+                events.append(pair)
+                pair = None
             if gat_obs is not None:
                 dist.all_gather_into_tensor(gat_obs, obs_buf[t])
                 dist.all_gather_into_tensor(gat_rew, rew_buf[t])
@@ -218,7 +218,7 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) / (T - 1)
 
     if world > 1:
         tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
@@ -230,7 +230,7 @@ def main():
     es = env.state_layout()[0]
     b_steady, b_avg = step_bytes(env.spec, es)
     achieved_gbs = (b_avg * n) / (kern_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(n)
+    traffic = pmc_traffic(n, env.kernel_info())
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -242,7 +242,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int32 state, f64 reward, f32 obs/actions",
+        "dtype": "%s state, f64 reward, f32 obs/actions" % ("int16" if es == 2 else "int32"),
         "data": "synthetic: in-kernel Philox4x32-10 Poisson(5) demand, uniform[-1,1] f32 actions (torch seed 0)",
         "config": {
             "workload": "C2 shape at the metric's size: MultiAgentInvManagement 4-stage serial "
@@ -259,9 +259,9 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "imenv_step_kernel<4,0,true,%s>" % ("short" if env.state_layout()[0] == 2 else "int"),
+            "kernel": env.kernel_info(),
             "kernel_us": round(kern_ms * 1e3, 3),
-            "kernel_samples": len(events),
+            "kernel_samples": len(events) * (T - 1),
             "bytes_per_env_step": round(b_avg, 3),
             "bytes_per_env_step_steady": b_steady,
             "bytes_per_launch": round(b_avg * n),

@@ -30,7 +30,9 @@
 #ifndef IMENV_H
 #define IMENV_H
 
+#ifndef __HIPCC_RTC__   /* hipRTC builds of the step kernel bring their own fixed-width types */
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -230,8 +232,26 @@ int imenv_dims(const ImEnv* env, int32_t* num_nodes, int32_t* num_features, int3
 int imenv_poisson_table(const ImEnv* env, uint32_t* out, int32_t cap, int32_t* len_out);
 
 /* Packed state layout chosen at create: element bytes (2 = int16 when the
- * spec's bounds prove every state value fits, else 4), row length per env, arrival-ring depth. */
+ * spec's bounds prove every state value fits, else 4), row length per env, and the rows of the
+ * in-transit ring (one row of n envs per node and lead-time slot: the sum of the delays). */
 int imenv_state_layout(const ImEnv* env, int32_t* elem_bytes, int32_t* row_len, int32_t* ring_depth);
+
+/* Step-kernel selection. mode 1 (the default; IMENV_JIT=0 in the environment makes 0 the
+ * default): step() runs a kernel compiled at run time with hipRTC for this spec, every spec value
+ * a compile-time constant (first step per dtype/layout combination pays ~1 s of compilation;
+ * cached per process). mode 0: the ahead-of-time kernels, which read the spec from device memory.
+ * Both compute the same function; a JIT failure falls back to mode 0 and is reported by
+ * imenv_kernel_info (IMENV_JIT_STRICT=1 turns it into an IMENV_E_UNSUPPORTED from step()). */
+int imenv_set_jit(ImEnv* env, int mode);
+
+/* NUL-terminated description of the kernel the last step() launched, truncated to len bytes. */
+int imenv_kernel_info(const ImEnv* env, char* buf, int64_t len);
+
+/* Diagnostics (no device needed): generate and compile with hipRTC the specialised step kernel of
+ * `spec` for `arch` (e.g. "gfx950"); flags = bit0 f64 actions, bit1 f64 obs, bit2 noisy delay,
+ * bit3 noisy demand, bit4 host-fed delay uniforms, bits 5+ demand layout. `log` receives "ok" or
+ * the compiler log. */
+int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, char* log, int64_t log_len);
 
 void imenv_destroy(ImEnv* env);
 

@@ -5,11 +5,14 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "imenv_device.h"
+#include "imenv_jit.h"
 
 using imenv::LaunchCfg;
 using imenv::SpecDev;
@@ -197,6 +200,8 @@ int validate_and_derive(const ImEnvSpec& s, SpecDev& d, int& maxc) {
       return fail(IMENV_E_UNSUPPORTED, "delay must be >= 1 in this build (delay 0 is a degenerate lead time)");
     if (s.delay[i] > IMENV_MAX_DELAY) return fail(IMENV_E_INVALID, "delay too large");
     if (s.delay[i] > d.dmax) d.dmax = s.delay[i];
+    d.ring_off[i] = d.ring_total;
+    d.ring_total += s.delay[i];
     if (s.inv_max[i] < 0 || s.order_max[i] < 0 || s.init_inv[i] < 0) return fail(IMENV_E_INVALID, "negative capacity");
     if (s.num_children[i] < 0 || s.num_children[i] > IMENV_MAX_CHILDREN)
       return fail(IMENV_E_UNSUPPORTED, "too many children");
@@ -315,6 +320,13 @@ struct ImEnv {
   bool have_delay_u = false;
   int demand_layout = IMENV_LAYOUT_DRAW;
   size_t demand_cap = 0;
+  // kernel selection (imenv_set_jit): hipRTC-specialised kernels per JitFlags, else ahead-of-time
+  int jit = 1;
+  bool jit_strict = false;   // IMENV_JIT_STRICT=1: a JIT failure is an error instead of an AOT fallback
+  std::string arch;
+  std::unordered_map<uint32_t, imenv::JitKernel> jit_k;
+  std::string jit_err;
+  std::string last_kernel;
 };
 
 extern "C" {
@@ -333,6 +345,8 @@ void imenv_destroy(ImEnv* h) {
                   h->d_episode};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  for (auto& kv : h->jit_k)
+    if (kv.second.mod) (void)hipModuleUnload(kv.second.mod);
   delete h;
 }
 
@@ -360,7 +374,7 @@ int imenv_create(const ImEnvSpec* spec, int64_t n_envs, int64_t env_offset, int 
   char **inv = reinterpret_cast<char**>(&h->d_inv), **bl = reinterpret_cast<char**>(&h->d_bl),
        **ou = reinterpret_cast<char**>(&h->d_ou), **ring = reinterpret_cast<char**>(&h->d_ring);
   if ((rc = alloc(&h->d_spec, 1)) || (rc = alloc(inv, rowb)) || (rc = alloc(bl, rowb)) || (rc = alloc(ou, rowb)) ||
-      (rc = alloc(ring, rowb * h->host.dmax)) || (rc = alloc(&h->d_carry, n * np)) ||
+      (rc = alloc(ring, n * h->es * h->host.ring_total)) || (rc = alloc(&h->d_carry, n * np)) ||
       (rc = alloc(&h->d_bto, h->maxc > 0 ? n * np : 0)) || (rc = alloc(&h->d_err, n)) ||
       (rc = alloc(&h->d_err_any, 1)) || (rc = alloc(&h->d_episode, 1))) {
     imenv_destroy(h);
@@ -387,6 +401,11 @@ int imenv_create(const ImEnvSpec* spec, int64_t n_envs, int64_t env_offset, int 
   if (he == hipSuccess) he = hipMemset(h->d_err_any, 0, sizeof(uint32_t));
   if (he == hipSuccess) he = hipMemset(h->d_episode, 0xFF, sizeof(uint32_t));   // first auto reset -> 0
   if (he != hipSuccess) { imenv_destroy(h); return fail(IMENV_E_HIP, std::string("init copy: ") + hipGetErrorString(he)); }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) h->arch = prop.gcnArchName;
+  if (h->arch.empty()) h->jit = 0;
+  if (const char* v = std::getenv("IMENV_JIT")) h->jit = (std::atoi(v) != 0 && !h->arch.empty()) ? 1 : 0;
+  if (const char* v = std::getenv("IMENV_JIT_STRICT")) h->jit_strict = std::atoi(v) != 0;
   *out = h;
   return IMENV_OK;
 }
@@ -481,9 +500,7 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
   A.noisy_delay_thr = h->noisy_thr;
   A.noisy_delay_thr32 = prob_thr32(h->noisy_thr);
   A.noisy_demand_thr32 = prob_thr32(s.noisy_demand_threshold);
-  const int D = h->host.dmax;
-  A.arr_row = h->t % D;
-  for (int i = 0; i < s.num_nodes; ++i) A.dep_row[i] = (h->t + s.delay[i]) % D;
+  for (int i = 0; i < s.num_nodes; ++i) A.ring_row[i] = h->host.ring_off[i] + h->t % s.delay[i];
   LaunchCfg c;
   c.mc = h->maxc;
   c.base = is_base_obs(s);
@@ -491,6 +508,46 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
   c.grid = (unsigned)((h->n + 255) / 256);
   c.stream = st;
   const int N = s.num_nodes;
+  if (h->jit) {
+    imenv::JitFlags f;
+    f.act_f64 = A.action_f64 != 0;
+    f.obs_f64 = A.obs_f64 != 0;
+    f.noisy_delay = A.noisy_delay != 0;
+    f.noisy_demand = A.noisy_demand != 0;
+    f.has_delay_u = A.delay_u != nullptr;
+    f.demand_layout = A.demand_layout;
+    auto it = h->jit_k.find(f.key());
+    if (it == h->jit_k.end()) {
+      // compiling + loading a module is not stream work: never do it while the stream is being
+      // captured into a graph (that launch takes the ahead-of-time kernel instead)
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      (void)hipStreamIsCapturing(st, &cs);
+      if (cs == hipStreamCaptureStatusNone) {
+        imenv::JitKernel k;
+        std::string msg;
+        if (imenv::jit_load(h->host, h->maxc, c.base, f, h->arch, k, msg)) {
+          it = h->jit_k.emplace(f.key(), k).first;
+        } else {
+          h->jit_err = msg;
+          if (h->jit_strict) return fail(IMENV_E_UNSUPPORTED, "JIT step kernel: " + msg);
+          h->jit = 0;   // recorded in imenv_kernel_info; the ahead-of-time kernels take over
+        }
+      }
+    }
+    if (it != h->jit_k.end()) {
+      HIPCHK(imenv::jit_launch(it->second, c.grid, st, h->d_spec, A));
+      h->last_kernel = it->second.tag;
+      h->t += 1;
+      if (done_out) *done_out = h->t >= s.num_periods ? 1 : 0;
+      return IMENV_OK;
+    }
+  }
+  {
+    char tag[96];
+    std::snprintf(tag, sizeof tag, "aot:imenv_step_kernel[NT=%d,MC=%d,base=%d,st16=%d]", N <= 8 ? N : 16, c.mc,
+                  c.base ? 1 : 0, c.st16 ? 1 : 0);
+    h->last_kernel = tag;
+  }
   switch (N) {   // exact kernels for N <= 8, padded NT = 16 above
     case 1: imenv::launch_step_nt<1>(c, h->d_spec, A); break;
     case 2: imenv::launch_step_nt<2>(c, h->d_spec, A); break;
@@ -583,7 +640,49 @@ int imenv_state_layout(const ImEnv* h, int32_t* elem_bytes, int32_t* row_len, in
   if (!h) return fail(IMENV_E_INVALID, "null handle");
   if (elem_bytes) *elem_bytes = (int32_t)h->es;
   if (row_len) *row_len = h->host.np;
-  if (ring_depth) *ring_depth = h->host.dmax;
+  if (ring_depth) *ring_depth = h->host.ring_total;
+  return IMENV_OK;
+}
+
+int imenv_set_jit(ImEnv* h, int mode) {
+  if (!h) return fail(IMENV_E_INVALID, "null handle");
+  if (mode != 0 && mode != 1) return fail(IMENV_E_INVALID, "mode must be 0 (ahead-of-time) or 1 (hipRTC)");
+  if (mode == 1 && h->arch.empty()) return fail(IMENV_E_UNSUPPORTED, "device architecture unknown");
+  h->jit = mode;
+  if (mode == 1) h->jit_err.clear();
+  return IMENV_OK;
+}
+
+int imenv_kernel_info(const ImEnv* h, char* buf, int64_t len) {
+  if (!h || !buf || len < 1) return fail(IMENV_E_INVALID, "null argument");
+  std::string s = h->last_kernel.empty() ? std::string(h->jit ? "jit (no step yet)" : "aot (no step yet)")
+                                         : h->last_kernel;
+  if (!h->jit_err.empty()) s += " | jit failed: " + h->jit_err;
+  std::snprintf(buf, (size_t)len, "%s", s.c_str());
+  return IMENV_OK;
+}
+
+int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, char* log, int64_t log_len) {
+  if (!spec || !arch) return fail(IMENV_E_INVALID, "null argument");
+  SpecDev d;
+  std::memset(&d, 0, sizeof(d));
+  int maxc = 0;
+  int rc = validate_and_derive(*spec, d, maxc);
+  if (rc != IMENV_OK) return rc;
+  std::vector<float> l32;
+  std::vector<double> l64;
+  build_obs_tables(d, l32, l64);
+  imenv::JitFlags f;
+  f.act_f64 = flags & 1u;
+  f.obs_f64 = flags & 2u;
+  f.noisy_delay = flags & 4u;
+  f.noisy_demand = flags & 8u;
+  f.has_delay_u = flags & 16u;
+  f.demand_layout = (int)(flags >> 5);
+  std::string msg;
+  auto code = imenv::jit_compile(imenv::jit_source(d, maxc, is_base_obs(*spec), f), arch, msg);
+  if (log && log_len > 0) std::snprintf(log, (size_t)log_len, "%s", code ? "ok" : msg.c_str());
+  if (!code) return fail(IMENV_E_UNSUPPORTED, "hipRTC: " + msg);
   return IMENV_OK;
 }
 

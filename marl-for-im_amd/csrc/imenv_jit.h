@@ -1,0 +1,57 @@
+// imenv_jit.h — run-time specialisation of the step kernel with hipRTC (host side).
+//
+// The ahead-of-time kernels (DynSpec) read every spec value from device memory. Specs are fixed for
+// the lifetime of a handle, so imenv_jit.hip instead writes the spec out as a policy class whose
+// accessors are all `static constexpr` (delays, capacities, prices, topology, observation map, the
+// Poisson inversion table, and the per-call flags), and compiles step_body against it with hipRTC:
+// every branch on the spec folds away, loops over nodes / children / features unroll to straight
+// code, and no scalar registers are spent holding spec values. One code object per (spec, flags,
+// arch) is cached for the process; modules are loaded per handle (device).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "imenv_device.h"
+
+namespace imenv {
+
+// Per-call properties the JIT kernel treats as compile-time constants.
+struct JitFlags {
+  bool act_f64 = false;
+  bool obs_f64 = false;
+  bool noisy_delay = false;
+  bool noisy_demand = false;
+  bool has_delay_u = false;
+  int demand_layout = IMENV_LAYOUT_DRAW;
+  uint32_t key() const {
+    return (act_f64 ? 1u : 0u) | (obs_f64 ? 2u : 0u) | (noisy_delay ? 4u : 0u) | (noisy_demand ? 8u : 0u) |
+           (has_delay_u ? 16u : 0u) | ((uint32_t)demand_layout << 5);
+  }
+};
+
+struct JitKernel {
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr;
+  std::string tag;    // short description (kernel_info)
+};
+
+// Policy + kernel source for one specialisation (maxc: widest split, base: inv/backlog/order_u obs).
+std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f);
+
+// Compile src with hipRTC for `arch` (e.g. "gfx950" or a device's gcnArchName); returns the code
+// object through the process-wide cache. On failure returns null and sets msg (compiler log).
+std::shared_ptr<const std::vector<char>> jit_compile(const std::string& src, const std::string& arch,
+                                                     std::string& msg);
+
+// Compile (cached) and load on the current device.
+bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const std::string& arch, JitKernel& out,
+              std::string& msg);
+
+hipError_t jit_launch(const JitKernel& k, unsigned grid, hipStream_t st, const SpecDev* sp, const StepArgs& A);
+
+}  // namespace imenv

@@ -72,6 +72,9 @@ SYMBOLS = [
     ("imenv_dims", c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     ("imenv_poisson_table", c_int, [c_void_p, POINTER(c_uint32), c_int32, POINTER(c_int32)]),
     ("imenv_state_layout", c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
+    ("imenv_set_jit", c_int, [c_void_p, c_int]),
+    ("imenv_kernel_info", c_int, [c_void_p, ctypes.c_char_p, c_int64]),
+    ("imenv_jit_check", c_int, [POINTER(ImEnvSpec), ctypes.c_char_p, c_uint32, ctypes.c_char_p, c_int64]),
     ("imenv_destroy", None, [c_void_p]),
     ("imenv_last_error", ctypes.c_char_p, []),
     ("imenv_abi_version", c_int, []),

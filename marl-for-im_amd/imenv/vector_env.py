@@ -180,10 +180,20 @@ class VectorInvEnv:
         return np.array(buf[:ln.value], dtype=np.uint64)
 
     def state_layout(self):
-        """(element bytes, row length, arrival-ring depth) of the packed HBM state."""
+        """(element bytes, packed row length, in-transit ring rows = sum of delays) of the HBM state."""
         eb, rl, rd = c_int32(), c_int32(), c_int32()
         nat.check(self.lib.imenv_state_layout(self._h, byref(eb), byref(rl), byref(rd)), "imenv_state_layout")
         return eb.value, rl.value, rd.value
+
+    def set_jit(self, mode):
+        """1: hipRTC kernel specialised for this spec (default); 0: ahead-of-time kernels."""
+        nat.check(self.lib.imenv_set_jit(self._h, int(mode)), "imenv_set_jit")
+
+    def kernel_info(self):
+        """Description of the kernel the last step() launched (and any JIT failure)."""
+        buf = ctypes.create_string_buffer(512)
+        nat.check(self.lib.imenv_kernel_info(self._h, buf, len(buf)), "imenv_kernel_info")
+        return buf.value.decode()
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:

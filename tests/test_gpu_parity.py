@@ -3,7 +3,12 @@
 All comparisons are exact: integer state/intermediates bit-equal; float64 obs and
 rewards bit-equal to the reference's float64 (IEEE ops in the reference's order,
 no FMA contraction); float32 obs equal to float32(reference obs).
+
+Every test runs twice: with the hipRTC-specialised step kernel ("jit", the default path) and with
+the ahead-of-time kernels ("aot"). IMENV_JIT_STRICT=1 makes a JIT failure an error, not a fallback.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -16,11 +21,21 @@ pytestmark = pytest.mark.gpu
 
 CASES = case_names()
 DEV = "cuda:0"
+os.environ["IMENV_JIT_STRICT"] = "1"
+MODE = {"kernel": "jit"}
+
+
+@pytest.fixture(autouse=True, params=["jit", "aot"])
+def kernel_mode(request):
+    MODE["kernel"] = request.param
+    yield request.param
 
 
 def _env(kind, cfg, n, **kw):
     from imenv import VectorInvEnv
-    return VectorInvEnv(kind, cfg, n_envs=n, device=DEV, **kw)
+    env = VectorInvEnv(kind, cfg, n_envs=n, device=DEV, **kw)
+    env.set_jit(1 if MODE["kernel"] == "jit" else 0)
+    return env
 
 
 def run_gpu_case(meta, d, obs_dtype=torch.float64, action_dtype=torch.float64):
@@ -47,6 +62,7 @@ def run_gpu_case(meta, d, obs_dtype=torch.float64, action_dtype=torch.float64):
         out["obs"].append(obs.cpu().numpy())
         r = rew.cpu().numpy()
         out["reward"].append(r if r.ndim == 2 else r[:, None])
+    assert env.kernel_info().startswith(MODE["kernel"] + ":"), env.kernel_info()
     flags, anyv = env.errors()
     env.close()
     return obs0, {k: np.stack(v, axis=1) for k, v in out.items()}, anyv

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc CSVs: per-kernel mean counter values per dispatch.
 
-    python tools/pmc_summary.py OUT.json DIR [DIR ...]
+    python tools/pmc_summary.py OUT.json N_ENVS DIR [DIR ...]
 
 Each DIR is one rocprofv3 -d output (one --pmc pass). Kernel names are shortened
 to their template head. If the calibration kernels (tools/pmc_calib.hip, 1 GiB per
@@ -23,6 +23,8 @@ def short(name):
     m = re.search(r"(imenv_\w+?)(<[^>]*>)?\(", name)
     if m:
         return m.group(1) + (m.group(2) or "")
+    if re.match(r"imenv_\w+$", name):       # extern "C" (hipRTC) kernels carry no signature
+        return name
     for k in ("read_dwordx4", "read_dword", "write_dwordx4", "write_dword"):
         if re.search(r"\b%s\b" % k, name):
             return k
@@ -47,15 +49,16 @@ def load(dirs):
 
 def main():
     outp = sys.argv[1]
-    s = load(sys.argv[2:])
-    res = {"kernels": s}
+    n_envs = int(sys.argv[2])
+    s = load(sys.argv[3:])
+    res = {"kernels": s, "n_envs": n_envs}
     fac = {}
     for k, c in (("read_dword", "FETCH_SIZE"), ("read_dwordx4", "FETCH_SIZE"), ("write_dword", "WRITE_SIZE"),
                  ("write_dwordx4", "WRITE_SIZE")):
         if k in s and c in s[k] and s[k][c] > 0:
             fac[k] = CAL_BYTES / (s[k][c] * 1024.0)
     res["bytes_per_counter_kb_factor"] = fac
-    step = [k for k in s if k.startswith("imenv_step_kernel")]
+    step = [k for k in s if k.startswith("imenv_step_kernel") or k.startswith("imenv_step_jit")]
     if step and "read_dword" in fac and "write_dword" in fac:
         k = step[0]
         c = s[k]
