@@ -535,7 +535,7 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
       }
     }
     if (it != h->jit_k.end()) {
-      HIPCHK(imenv::jit_launch(it->second, c.grid, st, h->d_spec, A));
+      HIPCHK(imenv::jit_launch(it->second, st, h->d_spec, A));
       h->last_kernel = it->second.tag;
       h->t += 1;
       if (done_out) *done_out = h->t >= s.num_periods ? 1 : 0;

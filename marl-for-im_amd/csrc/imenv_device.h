@@ -300,6 +300,7 @@ struct DynSpec {
   static constexpr bool EXACT = NT_ <= 8;    // AOT kernels for N <= 8 are compiled for N == NT
   static constexpr bool JIT = false;
   static constexpr int TAB_LDS = IMENV_TABLE_MAX;   // Poisson table staged in LDS
+  static constexpr int BS = 256;                     // threads (= envs) per block
   using ST = ST_;
   const SpecDev* __restrict__ sp;
   const StepArgs& A;
@@ -358,6 +359,9 @@ struct DynSpec {
   __device__ bool noisy_demand() const { return A.noisy_demand != 0; }
   __device__ bool has_delay_u() const { return A.delay_u != nullptr; }
   __device__ bool uses_hist() const { return A.hist_d != nullptr; }
+  // observation value of group g, node i for raw value v (table lookup, see obs_value32)
+  __device__ float obs32(int g, int i, int v, const float* __restrict__ lut) const;
+  __device__ double obs64(int g, int i, int v, const double* __restrict__ lut) const;
   // Poisson inversion: binary search over the LDS copy of the table
   __device__ int poisson_draw(uint32_t w, const uint32_t* s_tab) const {
     int lo = 0, hi = sp->table_len;
@@ -369,7 +373,7 @@ struct DynSpec {
   }
   __device__ void stage_tables(uint32_t* s_tab, bool poisson) const {
     if (poisson) {
-      for (int k = threadIdx.x; k < sp->table_len; k += 256) s_tab[k] = sp->table[k];
+      for (int k = threadIdx.x; k < sp->table_len; k += BS) s_tab[k] = sp->table[k];
       __syncthreads();
     }
   }
@@ -390,6 +394,17 @@ __device__ __forceinline__ float obs_value32(const P& p, const float* __restrict
   return (float)obs_map(p.group_mode(g), (double)v, p.a(), p.bma(), p.group_den(g, i), p.group_clip(g, i));
 }
 
+template <int NT_, int MC_, bool BASE_, typename ST_>
+__device__ __forceinline__ float DynSpec<NT_, MC_, BASE_, ST_>::obs32(int g, int i, int v,
+                                                                      const float* __restrict__ lut) const {
+  return obs_value32(*this, lut, g, i, v);
+}
+template <int NT_, int MC_, bool BASE_, typename ST_>
+__device__ __forceinline__ double DynSpec<NT_, MC_, BASE_, ST_>::obs64(int g, int i, int v,
+                                                                       const double* __restrict__ lut) const {
+  return obs_value64(*this, lut, g, i, v);
+}
+
 // ---------------------------------------------------------------- step body
 // Structure: (A) issue every load that does not depend on this step's arithmetic (raw words),
 // (B) compute in registers, (C) store; float32 BASE observations are staged through LDS so the
@@ -404,7 +419,8 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   using R = Row<ST, NT, EXACT>;
   using R32 = Row<int32_t, NT, EXACT>;
   const int tid = threadIdx.x;
-  const int64_t e0 = (int64_t)blockIdx.x * 256;
+  constexpr int BS = P::BS;
+  const int64_t e0 = (int64_t)blockIdx.x * BS;
   const int64_t e = e0 + tid;
   const int64_t n = A.n;
   const bool valid = e < n;
@@ -747,22 +763,22 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
           if (i < N) {
-            s_obs[tid * row + 3 * i + 0] = obs_value32(p, A.lut32, IMENV_G_INV, i, inv[i]);
-            s_obs[tid * row + 3 * i + 1] = obs_value32(p, A.lut32, IMENV_G_BACKLOG, i, bl[i]);
-            s_obs[tid * row + 3 * i + 2] = obs_value32(p, A.lut32, IMENV_G_ORDER_U, i, ou[i]);
+            s_obs[tid * row + 3 * i + 0] = p.obs32(IMENV_G_INV, i, inv[i], A.lut32);
+            s_obs[tid * row + 3 * i + 1] = p.obs32(IMENV_G_BACKLOG, i, bl[i], A.lut32);
+            s_obs[tid * row + 3 * i + 2] = p.obs32(IMENV_G_ORDER_U, i, ou[i], A.lut32);
           }
         }
       }
       __syncthreads();
-      const int64_t cnt = (n - e0) < 256 ? (n - e0) : 256;
+      const int64_t cnt = (n - e0) < BS ? (n - e0) : BS;
       const int64_t total = cnt * row;
       float* gobs = static_cast<float*>(A.obs) + e0 * row;
       if ((total & 3) == 0) {
         float4* g4 = reinterpret_cast<float4*>(gobs);
         const float4* s4 = reinterpret_cast<const float4*>(s_obs);
-        for (int64_t q = tid; q < total / 4; q += 256) g4[q] = s4[q];
+        for (int64_t q = tid; q < total / 4; q += BS) g4[q] = s4[q];
       } else {
-        for (int64_t q = tid; q < total; q += 256) gobs[q] = s_obs[q];
+        for (int64_t q = tid; q < total; q += BS) gobs[q] = s_obs[q];
       }
     } else if (valid) {
 #pragma unroll
@@ -771,14 +787,14 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           const int64_t base = (e * N + i) * 3;
           if (p.obs_f64()) {
             double* o = static_cast<double*>(A.obs);
-            o[base + 0] = obs_value64(p, A.lut64, IMENV_G_INV, i, inv[i]);
-            o[base + 1] = obs_value64(p, A.lut64, IMENV_G_BACKLOG, i, bl[i]);
-            o[base + 2] = obs_value64(p, A.lut64, IMENV_G_ORDER_U, i, ou[i]);
+            o[base + 0] = p.obs64(IMENV_G_INV, i, inv[i], A.lut64);
+            o[base + 1] = p.obs64(IMENV_G_BACKLOG, i, bl[i], A.lut64);
+            o[base + 2] = p.obs64(IMENV_G_ORDER_U, i, ou[i], A.lut64);
           } else {
             float* o = static_cast<float*>(A.obs);
-            o[base + 0] = obs_value32(p, A.lut32, IMENV_G_INV, i, inv[i]);
-            o[base + 1] = obs_value32(p, A.lut32, IMENV_G_BACKLOG, i, bl[i]);
-            o[base + 2] = obs_value32(p, A.lut32, IMENV_G_ORDER_U, i, ou[i]);
+            o[base + 0] = p.obs32(IMENV_G_INV, i, inv[i], A.lut32);
+            o[base + 1] = p.obs32(IMENV_G_BACKLOG, i, bl[i], A.lut32);
+            o[base + 2] = p.obs32(IMENV_G_ORDER_U, i, ou[i], A.lut32);
           }
         }
       }
@@ -831,8 +847,8 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
       for (int i = 0; i < NT; ++i) {
         if (i < N) {
           const int64_t idx = (e * N + i) * F + f;
-          if (p.obs_f64()) static_cast<double*>(A.obs)[idx] = obs_value64(p, A.lut64, g, i, v[i]);
-          else static_cast<float*>(A.obs)[idx] = obs_value32(p, A.lut32, g, i, v[i]);
+          if (p.obs_f64()) static_cast<double*>(A.obs)[idx] = p.obs64(g, i, v[i], A.lut64);
+          else static_cast<float*>(A.obs)[idx] = p.obs32(g, i, v[i], A.lut32);
         }
       }
     };
@@ -849,12 +865,12 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
 // obs staging buffer size (floats) for a policy
 template <class P>
 constexpr int stage_floats() {
-  return (P::BASE && P::NT <= 8) ? 256 * 3 * P::NT : 4;
+  return (P::BASE && P::NT <= 8) ? P::BS * 3 * P::NT : 4;
 }
 
 // Kernel template for any policy whose constructor takes (spec, args).
 template <class P>
-__global__ void __launch_bounds__(256) imenv_step_kernel(const SpecDev* __restrict__ sp, const StepArgs A) {
+__global__ void __launch_bounds__(P::BS) imenv_step_kernel(const SpecDev* __restrict__ sp, const StepArgs A) {
   __shared__ uint32_t s_tab[P::TAB_LDS];
   __shared__ __attribute__((aligned(16))) float s_obs[stage_floats<P>()];
   const P p(sp, A);

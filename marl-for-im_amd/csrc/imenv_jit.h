@@ -37,6 +37,7 @@ struct JitFlags {
 struct JitKernel {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr;
+  int bs = 256;       // threads (= envs) per block
   std::string tag;    // short description (kernel_info)
 };
 
@@ -52,6 +53,6 @@ std::shared_ptr<const std::vector<char>> jit_compile(const std::string& src, con
 bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const std::string& arch, JitKernel& out,
               std::string& msg);
 
-hipError_t jit_launch(const JitKernel& k, unsigned grid, hipStream_t st, const SpecDev* sp, const StepArgs& A);
+hipError_t jit_launch(const JitKernel& k, hipStream_t st, const SpecDev* sp, const StepArgs& A);
 
 }  // namespace imenv

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <mutex>
 #include <sstream>
@@ -56,6 +57,80 @@ const char* blit(bool b) { return b ? "true" : "false"; }
 
 constexpr int kInlineTable = 64;   // Poisson tables up to this length become a compare-sum
 
+// Threads (= envs) per block of the JIT kernel: 256 measured best for the C2 kernel (25.8 us vs
+// 26.3 us at 512 and 27.6 us at 1024, profiles/r01); IMENV_JIT_BS overrides (64..1024, multiple of 64).
+int jit_block_size() {
+  int bs = 256;
+  if (const char* v = std::getenv("IMENV_JIT_BS")) bs = std::atoi(v);
+  if (bs < 64 || bs > 1024 || bs % 64) bs = 256;
+  return bs;
+}
+
+// The reference's observation value a + (v * (b - a)) / den (IM_env.py:435-444), in the same IEEE
+// double expression as the device's obs_map (both built with -ffp-contract=off).
+double ref_obs(const ImEnvSpec& s, int g, int i, int v) {
+  double x = (double)v;
+  if (s.group_mode[g] == IMENV_OBS_CLAMP_SCALED) x = std::fmin(x, s.group_clip[g][i]);
+  return s.a + (x * (s.b - s.a)) / s.group_den[g][i];
+}
+
+std::string flit(float x) {
+  char buf[64];
+  std::snprintf(buf, sizeof buf, "(%af)", (double)x);
+  return buf;
+}
+
+// Observation hooks. The tabulated range [0, lut_max] of every scaled (group, node) is small, so the
+// generator tries cheap closed forms and keeps one only if it reproduces the reference expression
+// bit for bit at EVERY value of that range (exhaustive check here, on the host); anything else,
+// and values outside the range, go through the lookup table / full expression. With one FMA per
+// value the kernel avoids a dependent round trip of table gathers after its arithmetic.
+void emit_obs_hooks(std::ostream& o, const SpecDev& d) {
+  const ImEnvSpec& s = d.s;
+  const bool use = !(std::getenv("IMENV_JIT_OBS") && std::string(std::getenv("IMENV_JIT_OBS")) == "lut");
+  std::ostringstream c32, c64;
+  for (int g = 0; g < IMENV_NUM_GROUPS && use; ++g) {
+    const int mode = s.group_mode[g];
+    if (mode != IMENV_OBS_SCALED && mode != IMENV_OBS_CLAMP_SCALED) continue;
+    for (int i = 0; i < s.num_nodes; ++i) {
+      const int mx = d.lut_max[g][i];
+      if (mx < 0) continue;
+      const double d1 = (s.b - s.a) / s.group_den[g][i];
+      const float c1 = (float)d1, c0 = (float)s.a;
+      bool k1 = true, k2 = true, k3 = true, q1 = true, q2 = true;
+      for (int v = 0; v <= mx; ++v) {
+        const double e = ref_obs(s, g, i, v);
+        const float e32 = (float)e;
+        const float r1 = std::fmaf((float)v, c1, c0);
+        const float r2 = (float)std::fma((double)v, d1, s.a);
+        const float r3 = (float)((double)v * d1 + s.a);
+        k1 = k1 && std::memcmp(&r1, &e32, 4) == 0;
+        k2 = k2 && std::memcmp(&r2, &e32, 4) == 0;
+        k3 = k3 && std::memcmp(&r3, &e32, 4) == 0;
+        const double s1 = std::fma((double)v, d1, s.a);
+        const double s2 = (double)v * d1 + s.a;
+        q1 = q1 && std::memcmp(&s1, &e, 8) == 0;
+        q2 = q2 && std::memcmp(&s2, &e, 8) == 0;
+      }
+      const std::string guard = "if ((unsigned)v <= " + std::to_string(mx) + "u) return ";
+      const std::string cs = "    case " + std::to_string(g * 256 + i) + ": ";
+      if (k1) c32 << cs << guard << "__builtin_fmaf((float)v, " << flit(c1) << ", " << flit(c0) << "); break;\n";
+      else if (k2) c32 << cs << guard << "(float)__builtin_fma((double)v, " << dlit(d1) << ", " << dlit(s.a) << "); break;\n";
+      else if (k3) c32 << cs << guard << "(float)((double)v * " << dlit(d1) << " + " << dlit(s.a) << "); break;\n";
+      if (q1) c64 << cs << guard << "__builtin_fma((double)v, " << dlit(d1) << ", " << dlit(s.a) << "); break;\n";
+      else if (q2) c64 << cs << guard << "(double)v * " << dlit(d1) << " + " << dlit(s.a) << "; break;\n";
+    }
+  }
+  o << "  __device__ float obs32(int g, int i, int v, const float* __restrict__ lut) const {\n"
+       "    switch (g * 256 + i) {\n"
+    << c32.str()
+    << "    default: break;\n    }\n    return imenv::obs_value32(*this, lut, g, i, v);\n  }\n";
+  o << "  __device__ double obs64(int g, int i, int v, const double* __restrict__ lut) const {\n"
+       "    switch (g * 256 + i) {\n"
+    << c64.str()
+    << "    default: break;\n    }\n    return imenv::obs_value64(*this, lut, g, i, v);\n  }\n";
+}
+
 }  // namespace
 
 std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f) {
@@ -76,6 +151,7 @@ std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f)
     << "  static constexpr bool EXACT = true;\n"
     << "  static constexpr bool JIT = true;\n"
     << "  static constexpr int TAB_LDS = " << (inline_tab ? 1 : IMENV_TABLE_MAX) << ";\n"
+    << "  static constexpr int BS = " << jit_block_size() << ";\n"
     << "  using ST = " << (d.st16 ? "int16_t" : "int32_t") << ";\n"
     << "  const imenv::SpecDev* __restrict__ sp;\n"
     << "  __device__ JitSpec(const imenv::SpecDev* __restrict__ s, const imenv::StepArgs&) : sp(s) {}\n";
@@ -139,6 +215,7 @@ std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f)
         "(0.0)");
   emit2(o, "int", "lut_max", IMENV_NUM_GROUPS, N, [&](int g, int i) { return ilit(d.lut_max[g][i]); }, "-1");
   emit2(o, "int", "lut_off", IMENV_NUM_GROUPS, N, [&](int g, int i) { return ilit(d.lut_off[g][i]); }, "0");
+  emit_obs_hooks(o, d);
   if (inline_tab) {
     // count of thresholds <= w == searchsorted(table, w, 'right') for the sorted table
     o << "  __device__ static int poisson_draw(uint32_t w, const uint32_t*) {\n    int k = 0;\n";
@@ -157,7 +234,7 @@ std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f)
       << d.table_len << "; k += 256) s_tab[k] = sp->table[k]; __syncthreads(); }\n  }\n";
   }
   o << "};\n\n"
-       "extern \"C\" __global__ void __launch_bounds__(256)\n"
+       "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
        "imenv_step_jit(const imenv::SpecDev* __restrict__ sp, const imenv::StepArgs A) {\n"
        "  __shared__ uint32_t s_tab[JitSpec::TAB_LDS];\n"
        "  __shared__ __attribute__((aligned(16))) float s_obs[imenv::stage_floats<JitSpec>()];\n"
@@ -254,18 +331,20 @@ bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const st
   }
   out.mod = mod;
   out.fn = fn;
+  out.bs = jit_block_size();
   char tag[160];
-  std::snprintf(tag, sizeof tag, "jit:imenv_step_jit[N=%d,MC=%d,base=%d,st16=%d,flags=0x%x,%zuB]", d.s.num_nodes,
-                maxc, base ? 1 : 0, d.st16, f.key(), src.size());
+  std::snprintf(tag, sizeof tag, "jit:imenv_step_jit[N=%d,MC=%d,base=%d,st16=%d,flags=0x%x,bs=%d,%zuB]",
+                d.s.num_nodes, maxc, base ? 1 : 0, d.st16, f.key(), out.bs, src.size());
   out.tag = tag;
   return true;
 }
 
-hipError_t jit_launch(const JitKernel& k, unsigned grid, hipStream_t st, const SpecDev* sp, const StepArgs& A) {
+hipError_t jit_launch(const JitKernel& k, hipStream_t st, const SpecDev* sp, const StepArgs& A) {
   const SpecDev* spv = sp;
   StepArgs av = A;
   void* args[] = {&spv, &av};
-  return hipModuleLaunchKernel(k.fn, grid, 1, 1, 256, 1, 1, 0, st, args, nullptr);
+  const unsigned grid = (unsigned)((A.n + k.bs - 1) / k.bs);
+  return hipModuleLaunchKernel(k.fn, grid, 1, 1, (unsigned)k.bs, 1, 1, 0, st, args, nullptr);
 }
 
 }  // namespace imenv
