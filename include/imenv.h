@@ -236,6 +236,14 @@ int imenv_poisson_table(const ImEnv* env, uint32_t* out, int32_t cap, int32_t* l
  * in-transit ring (one row of n envs per node and lead-time slot: the sum of the delays). */
 int imenv_state_layout(const ImEnv* env, int32_t* elem_bytes, int32_t* row_len, int32_t* ring_depth);
 
+/* Host-fed noisy-delay uniforms for ONE period (device double [N][n]) written into the table that
+ * reset(delay_uniforms=...) fills, so a caller can draw them lazily, step by step, in the
+ * reference's order (np.random.uniform per node, factory first, IM_env.py:384-407) and keep its
+ * host RNG stream identical to the reference even across mid-episode resets. period must be >= the
+ * current period. Rows never written read as 1.0. Switches the handle to host-fed uniforms until
+ * the next reset() without a table. */
+int imenv_set_delay_uniforms(ImEnv* env, int32_t period, const double* u, void* stream);
+
 /* Step-kernel selection. mode 1 (the default; IMENV_JIT=0 in the environment makes 0 the
  * default): step() runs a kernel compiled at run time with hipRTC for this spec, every spec value
  * a compile-time constant (first step per dtype/layout combination pays ~1 s of compilation;

@@ -644,6 +644,30 @@ int imenv_state_layout(const ImEnv* h, int32_t* elem_bytes, int32_t* row_len, in
   return IMENV_OK;
 }
 
+int imenv_set_delay_uniforms(ImEnv* h, int32_t period, const double* u, void* stream) {
+  if (!h || !u) return fail(IMENV_E_INVALID, "null argument");
+  if (!h->reset_done) return fail(IMENV_E_NOT_RESET, "set_delay_uniforms() before reset()");
+  const ImEnvSpec& s = h->host.s;
+  if (period < h->t || period >= s.num_periods)
+    return fail(IMENV_E_INVALID, "period must lie in [current period, num_periods)");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  HIPCHK(hipSetDevice(h->device));
+  const size_t T = s.num_periods, N = s.num_nodes, n = h->n;
+  if (!h->d_delay_u) {
+    int rc = alloc(&h->d_delay_u, T * N * n);
+    if (rc) return rc;
+  }
+  if (!h->have_delay_u) {   // rows not written by the caller read as 1.0 (no extra delay unless thr >= 1)
+    std::vector<double> ones(T * N * n, 1.0);
+    HIPCHK(hipMemcpyAsync(h->d_delay_u, ones.data(), ones.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    h->have_delay_u = true;
+  }
+  HIPCHK(hipMemcpyAsync(h->d_delay_u + (size_t)period * N * n, u, N * n * sizeof(double), hipMemcpyDeviceToDevice,
+                        st));
+  return IMENV_OK;
+}
+
 int imenv_set_jit(ImEnv* h, int mode) {
   if (!h) return fail(IMENV_E_INVALID, "null handle");
   if (mode != 0 && mode != 1) return fail(IMENV_E_INVALID, "mode must be 0 (ahead-of-time) or 1 (hipRTC)");

@@ -72,6 +72,7 @@ SYMBOLS = [
     ("imenv_dims", c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     ("imenv_poisson_table", c_int, [c_void_p, POINTER(c_uint32), c_int32, POINTER(c_int32)]),
     ("imenv_state_layout", c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
+    ("imenv_set_delay_uniforms", c_int, [c_void_p, c_int32, c_void_p, c_void_p]),
     ("imenv_set_jit", c_int, [c_void_p, c_int]),
     ("imenv_kernel_info", c_int, [c_void_p, ctypes.c_char_p, c_int64]),
     ("imenv_jit_check", c_int, [POINTER(ImEnvSpec), ctypes.c_char_p, c_uint32, ctypes.c_char_p, c_int64]),

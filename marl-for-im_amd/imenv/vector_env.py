@@ -128,6 +128,13 @@ class VectorInvEnv:
         self.episode = self.episode + 1 if episode is None else int(episode)
         return obs
 
+    def set_delay_uniforms(self, period, u):
+        """Host-fed noisy-delay uniforms [n, N] (float64) for one period (imenv_set_delay_uniforms)."""
+        t = torch.as_tensor(u).to(device=self.device, dtype=torch.float64).reshape(self.n, self.N).t().contiguous()
+        nat.check(self.lib.imenv_set_delay_uniforms(self._h, int(period), t.data_ptr(), self._stream()),
+                  "imenv_set_delay_uniforms")
+        self._keep_u = t
+
     def step(self, actions, obs_out=None, reward_out=None, info=False):
         """step(action) (IM_env.py:287-360): actions [n, N] (or [n*N]) in the spec's action units."""
         a = actions if torch.is_tensor(actions) else torch.as_tensor(np.asarray(actions))

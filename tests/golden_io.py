@@ -35,3 +35,14 @@ def load_case(name):
 def load_kat():
     with open(os.path.join(GOLDEN, "kat.json")) as f:
         return json.load(f)
+
+
+def adaptor_case_names():
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "adaptor", "*.npz")))
+
+
+def load_adaptor_case(name):
+    z = np.load(os.path.join(GOLDEN, "adaptor", name + ".npz"), allow_pickle=False)
+    d = {k: z[k] for k in z.files}
+    meta = json.loads(str(d.pop("meta")))
+    return meta, d

@@ -9,7 +9,7 @@ not installed here (gym.Env / gym.spaces.Box and ray.rllib.MultiAgentEnv carry n
 arithmetic), steps every env with host-fed demand and actions, and records the
 per-period history. Nothing from the reference is copied: the outputs are data.
 
-    python tools/gen_fixtures.py            # writes tests/golden/*.npz + kat.json
+    python tools/gen_fixtures.py            # writes tests/golden/*.npz, kat.json, adaptor/*.npz
 
 Each case: E envs x T periods. Recorded (per period, after the step):
 order, demand, acquisition, ship, inv, backlog, order_u, obs, reward, profit,
@@ -334,6 +334,95 @@ def kats(classes):
     return out
 
 
+# ----------------------------------------------------------------- adaptor traces
+# Scripted sessions with the reference's OWN randomness (np.random.seed in the constructor, scipy
+# demand draws at reset, noisy-delay / noisy-demand uniforms on the global stream): construct,
+# run the constructor's episode, reset, run 10 steps, reset mid-episode (optionally latching noisy
+# delay), run a full episode. Actions come from a separate RandomState so the global stream is the
+# env's alone. tests/test_adaptors_gpu.py replays the same script on imenv.envs.
+ADAPTOR_CASES = {
+    "ad_IM4_mu3": ("IM", serial4(mu=3), {}),
+    "ad_IM4_custom": ("IM", serial4(demand_dist="custom", customer_demand=np.arange(30) % 7), {}),
+    "ad_IM4_noisy": ("IM", serial4(time_dependency=True), {"noisy": 0.3}),
+    "ad_MAIM4_mu3": ("MAIM", serial4(independent=False, mu=3), {}),
+    "ad_MAIM4_uniform_indep_noisy": ("MAIM", serial4(independent=True, demand_dist="uniform",
+                                                     lower_upper=(2, 7), time_dependency=True), {"noisy": 0.4}),
+    "ad_IM_div1_noisy_demand": ("IM_div", div1(noisy_demand=True, noisy_demand_threshold=0.2,
+                                               time_dependency=True), {}),
+    "ad_MAIM_div1_cfg_noisy_delay": ("MAIM_div", div1(time_dependency=True, prev_demand=True, noisy_delay=True,
+                                                      noisy_delay_threshold=0.25), {}),
+    "ad_MAIM_div2_share": ("MAIM_div", div2(share_network=True, time_dependency=True), {}),
+}
+
+
+def adaptor_script(env, kind, opts, rs, record):
+    """The session both the reference and the adaptor run (tests/test_adaptors_gpu.py)."""
+    ma = kind in ("MAIM", "MAIM_div")
+    prefix = "stage_" if kind == "MAIM" else "node_"
+    N = env.num_nodes if hasattr(env, "num_nodes") else env.num_stages
+    T = env.num_periods
+    record("reset", env.state, env.customer_demand)
+
+    def run(steps):
+        for _ in range(steps):
+            x = rs.uniform(-1.05, 1.05, size=N)
+            act = {prefix + str(i): np.array([x[i]]) for i in range(N)} if ma else x
+            out = env.step(act)
+            record("step", *out)
+
+    run(T)
+    record("reset", env.reset(), env.customer_demand)
+    run(10)
+    if "noisy" in opts:
+        record("reset", env.reset(noisy_delay=True, noisy_delay_threshold=opts["noisy"]), env.customer_demand)
+    else:
+        record("reset", env.reset(), env.customer_demand)
+    run(T)
+
+
+def adaptor_traces(classes):
+    for name, (kind, cfg, opts) in ADAPTOR_CASES.items():
+        ma = kind in ("MAIM", "MAIM_div")
+        caller = dict(cfg)
+        env = classes[kind](caller)
+        rec = {"reset_obs": [], "reset_demand": [], "obs": [], "reward": [], "done": [], "period": [],
+               "demand": [], "ship": [], "acquisition": [], "profit": [], "actual_order": []}
+        N = env.num_nodes if hasattr(env, "num_nodes") else env.num_stages
+
+        def record(what, *args):
+            if what == "reset":
+                rec["reset_obs"].append(obs_array(args[0], ma, N))
+                rec["reset_demand"].append(np.asarray(args[1], dtype=np.int64).reshape(-1))
+                return
+            obs, r, d, info = args
+            rec["obs"].append(obs_array(obs, ma, N))
+            if ma:
+                keys = sorted(r.keys(), key=lambda s: int(s.split("_")[1]))
+                rec["reward"].append(np.array([r[k] for k in keys], dtype=np.float64))
+                rec["done"].append(bool(d["__all__"]))
+                ik = sorted(info.keys(), key=lambda s: int(s.split("_")[1]))
+                rec["period"].append(info[ik[0]]["period"])
+                for f, src in (("demand", "demand"), ("ship", "ship"), ("acquisition", "acquisition"),
+                               ("profit", "profit"), ("actual_order", "actual order")):
+                    rec[f].append(np.array([info[k][src] for k in ik], dtype=np.float64))
+            else:
+                rec["reward"].append(np.array([r], dtype=np.float64))
+                rec["done"].append(bool(d))
+                rec["period"].append(info["period"])
+                for f in ("demand", "ship", "acquisition", "profit"):
+                    rec[f].append(np.asarray(info[f], dtype=np.float64).copy())
+                rec["actual_order"].append(np.zeros(N))
+
+        adaptor_script(env, kind, opts, np.random.RandomState(7), record)
+        out = {k: np.array(v) for k, v in rec.items() if k != "reset_demand"}
+        out["reset_demand"] = np.array(rec["reset_demand"])
+        out["meta"] = json.dumps(dict(kind=kind, config=jsonable(cfg), opts=opts,
+                                      caller_keys_after=sorted(caller.keys())))
+        os.makedirs(os.path.join(OUT, "adaptor"), exist_ok=True)
+        np.savez_compressed(os.path.join(OUT, "adaptor", name + ".npz"), **out)
+        print("%-30s %-9s steps=%d" % (name, kind, len(rec["obs"])))
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference not mounted; nothing to do (fixtures are committed)")
@@ -346,6 +435,7 @@ def main():
         print("%-26s %-9s errs=%d" % (name, kind, int((out["err"] >= 0).sum())))
     with open(os.path.join(OUT, "kat.json"), "w") as f:
         json.dump(kats(classes), f, indent=1)
+    adaptor_traces(classes)
 
 
 if __name__ == "__main__":
