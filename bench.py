@@ -150,6 +150,7 @@ def main():
     import torch.distributed as dist
     from imenv import VectorInvEnv
     from imenv import _native as nat
+    from imenv.shard import StepGather, weak_offset
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -157,7 +158,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     n = args.n_envs
-    env = VectorInvEnv("MAIM", C2_CONFIG, n_envs=n, device=dev, env_offset=rank * n)
+    env = VectorInvEnv("MAIM", C2_CONFIG, n_envs=n, device=dev, env_offset=weak_offset(n, rank))
     N, F, T = env.N, env.F, env.T
     g = torch.Generator(device=dev)
     g.manual_seed(0)
@@ -165,10 +166,9 @@ def main():
     obs_buf = torch.empty((T, n, N, F), dtype=torch.float32, device=dev)
     obs0 = torch.empty((n, N, F), dtype=torch.float32, device=dev)
     rew_buf = torch.empty((T, n), dtype=torch.float64, device=dev)
-    gat_obs = gat_rew = None
+    gather = None
     if args.gather and world > 1:
-        gat_obs = torch.empty((world * n, N, F), dtype=torch.float32, device=dev)
-        gat_rew = torch.empty((world * n,), dtype=torch.float64, device=dev)
+        gather = StepGather(obs_buf[0], rew_buf[0])
 
     lib, h = env.lib, env._h
     stream = torch.cuda.current_stream(dev)
@@ -198,9 +198,8 @@ def main():
                 pair[1].record(stream)
                 events.append(pair)
                 pair = None
-            if gat_obs is not None:
-                dist.all_gather_into_tensor(gat_obs, obs_buf[t])
-                dist.all_gather_into_tensor(gat_rew, rew_buf[t])
+            if gather is not None:
+                gather(obs_buf[t], rew_buf[t])
 
     # warmup (whole episodes so the timed region starts at a reset)
     w = ((args.warmup + T - 1) // T) * T
@@ -224,6 +223,22 @@ def main():
         tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el, kern_ms = tt[0].item(), tt[1].item()
+
+    # measured stream-copy ceiling at the step's byte count: a device copy of half the
+    # bytes moves them once in and once out; outside the timed region
+    half = max(1 << 20, int(step_bytes(env.spec, env.state_layout()[0])[1] * n) // 2 // 16 * 16)
+    csrc = torch.empty(half // 4, dtype=torch.float32, device=dev)
+    cdst = torch.empty_like(csrc)
+    for _ in range(3):
+        cdst.copy_(csrc)
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    c0.record(stream)
+    for _ in range(20):
+        cdst.copy_(csrc)
+    c1.record(stream)
+    c1.synchronize()
+    copy_gbs = 2 * half * 20 / (c0.elapsed_time(c1) * 1e-3) / 1e9
+    del csrc, cdst
 
     total_env_steps = world * n * K
     value = total_env_steps / el
@@ -250,7 +265,7 @@ def main():
                         "30-period episodes with the reset inside the timed loop",
             "n_envs_per_gpu": n, "global_envs": world * n, "num_stages": N, "obs_features": F,
             "num_periods": T, "parallelism": "env-sharded x%d (one process per GPU, no data-path collective%s)"
-                                             % (world, ", + RCCL all-gather of obs/reward per step" if gat_obs is not None else ""),
+                                             % (world, ", + RCCL all-gather of obs/reward per step" if gather is not None else ""),
         },
         "roofline": {
             "bound": "hbm",
@@ -259,6 +274,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "copy_ceiling_gbs": round(copy_gbs, 1),
             "kernel": env.kernel_info(),
             "kernel_us": round(kern_ms * 1e3, 3),
             "kernel_samples": len(events) * (T - 1),

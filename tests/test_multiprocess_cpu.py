@@ -1,0 +1,105 @@
+"""World-size-2 gloo runs of the sharded path on CPU.
+
+Each rank owns a contiguous range of global env ids (imenv.shard), draws demand keyed by the
+GLOBAL id (the oracle's Philox twin of the kernel's draws), steps its shard and all-gathers every
+step's obs and reward with imenv.shard.StepGather (the same helper bench.py --gather uses with
+RCCL). Rank 0's gathered trajectory must equal one single-process run over all envs, which is what
+makes the GPU count invisible in the results.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from imenv.shard import StepGather, shard_range, weak_offset
+
+C2 = dict(num_stages=4, num_periods=30, init_inv=np.ones(4) * 10, inv_target=np.zeros(4),
+          inv_max=np.ones(4) * 30, price=np.array([5, 4, 3, 2, 1]),
+          stock_cost=np.array([0.35, 0.3, 0.4, 0.2]), backlog_cost=np.array([0.5, 0.7, 0.6, 0.9]),
+          delay=np.array([1, 2, 3, 1]), demand_dist="poisson", mu=5, seed=52, independent=False)
+C4 = dict(num_nodes=4, connections={0: [1], 1: [2, 3], 2: [], 3: []}, num_periods=30,
+          init_inv=np.ones(4) * 10, inv_target=np.zeros(4), inv_max=np.ones(4) * 30,
+          stock_cost=np.array([0.35, 0.3, 0.4, 0.4]), backlog_cost=np.array([0.5, 0.7, 0.6, 0.6]),
+          delay=np.array([1, 2, 1, 1]), demand_dist="poisson", mu=5, seed=52, time_dependency=True,
+          prev_demand=True, independent=True)
+N_TOTAL = 96
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _actions(kind, n_total, T):
+    rs = np.random.RandomState(11)
+    return rs.uniform(-1.1, 1.1, size=(T, n_total, 4)).astype(np.float32).astype(np.float64)
+
+
+def _rollout(kind, cfg, offset, count, acts, gather=None):
+    from oracle.im_oracle import OracleEnv
+    env = OracleEnv(kind, cfg, n_envs=count)
+    obs_all, rew_all = [], []
+    for ep in range(2):
+        env.reset(rng=dict(seed=52, episode=ep, env_offset=offset, dist="poisson", mu=5))
+        for t in range(30):
+            obs, rew, _, _ = env.step(acts[t, offset:offset + count])
+            o, r = torch.from_numpy(np.ascontiguousarray(obs)), torch.from_numpy(np.ascontiguousarray(rew))
+            if gather is not None:
+                o, r = gather(o, r)
+            obs_all.append(o.clone())
+            rew_all.append(r.clone())
+    return torch.stack(obs_all), torch.stack(rew_all)
+
+
+def _worker(rank, world, port, kind, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = C2 if kind == "MAIM" else C4
+        offset, count = shard_range(N_TOTAL, world, rank)
+        acts = _actions(kind, N_TOTAL, 30)
+        from oracle.im_oracle import OracleEnv
+        probe = OracleEnv(kind, cfg, n_envs=count)
+        o0 = probe.reset(rng=dict(seed=52, episode=0, env_offset=offset, dist="poisson", mu=5))
+        r_shape = (count,) + ((4,) if kind == "MAIM_div" else ())
+        g = StepGather(torch.zeros((count,) + o0.shape[1:], dtype=torch.float64),
+                       torch.zeros(r_shape, dtype=torch.float64))
+        obs, rew = _rollout(kind, cfg, offset, count, acts, gather=g)
+        # timing contract of bench.py: max over ranks
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if rank == 0:
+            torch.save(dict(obs=obs, rew=rew, tmax=t), out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["MAIM", "MAIM_div"])
+def test_two_rank_gather_equals_single_run(kind, tmp_path):
+    out = str(tmp_path / "rank0.pt")
+    mp.spawn(_worker, args=(2, _free_port(), kind, out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    cfg = C2 if kind == "MAIM" else C4
+    ref_obs, ref_rew = _rollout(kind, cfg, 0, N_TOTAL, _actions(kind, N_TOTAL, 30))
+    assert torch.equal(got["obs"], ref_obs)
+    assert torch.equal(got["rew"], ref_rew)
+    assert got["tmax"].item() == 2.0
+
+
+def test_shard_range_partitions_ids():
+    for total in (1, 7, 96, 1 << 20):
+        for world in (1, 2, 3, 8):
+            if total < world:
+                continue
+            spans = [shard_range(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0
+            assert sum(c for _, c in spans) == total
+            for (o1, c1), (o2, _) in zip(spans, spans[1:]):
+                assert o1 + c1 == o2
+            assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+    assert weak_offset(1 << 20, 3) == 3 << 20
