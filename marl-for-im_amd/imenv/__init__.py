@@ -1,7 +1,8 @@
 """imenv — MI355X-native vectorised inventory-management environment.
 
-Host side of the hot path: a HIP kernel library (csrc/imenv_kernels.hip, C ABI in
-include/imenv.h) driven from Python. Public surface:
+Host side of the hot path: a HIP kernel library (csrc/: the step kernel body imenv_device.h,
+ahead-of-time instantiations imenv_step_nt*.hip, the hipRTC specialiser imenv_jit.hip and the C ABI
+imenv_capi.hip; declared in include/imenv.h) driven from Python. Public surface:
 
   build_spec(kind, config)      reference config dict -> HostSpec (spec.py)
   VectorInvEnv(kind, config, n) batched envs on one GPU (vector_env.py)

@@ -1,8 +1,8 @@
 """Philox4x32-10 counter RNG and the demand samplers built on it — NumPy restatement.
 
 TEST INFRASTRUCTURE ONLY (see oracle/__init__.py). The product draws the same
-numbers inside the HIP step kernel (marl-for-im_amd/csrc/imenv_kernels.hip,
-``philox4x32_10`` / ``draw_demand``); this module lets the tests check those
+numbers inside the HIP step kernel (marl-for-im_amd/csrc/imenv_device.h,
+``philox_word`` and the demand block of ``step_body``); this module lets the tests check those
 in-kernel draws bit-exactly on the CPU.
 
 Why this exists: the reference draws the whole demand horizon at ``reset()`` from
@@ -15,7 +15,7 @@ so every env's stream is independent of how envs are sharded over GPUs.
 
 Algorithm (Salmon et al., "Parallel random numbers: as easy as 1, 2, 3", SC'11;
 Random123 ``philox4x32_R(10, ...)``), pinned by the published known-answer vectors
-in tests/test_oracle_rng.py.
+in tests/test_oracle_golden.py (KAT tests).
 
 Counter layout used by the product (all uint32):
     c0 = global env id, c1 = episode, c2 = period t, c3 = (stream << 16) | block
