@@ -231,8 +231,8 @@ int imenv_dims(const ImEnv* env, int32_t* num_nodes, int32_t* num_features, int3
  * buffer of capacity `cap`); *len_out receives the table length. */
 int imenv_poisson_table(const ImEnv* env, uint32_t* out, int32_t cap, int32_t* len_out);
 
-/* Packed state layout chosen at create: element bytes (2 = int16 when the
- * spec's bounds prove every state value fits, else 4), row length per env, and the rows of the
+/* Packed state layout chosen at create: element bytes (1 = uint8 / 2 = int16 when
+ * the spec's bounds prove every state value fits in 0..255 / 32767, else 4), row length per env, and the rows of the
  * in-transit ring (one row of n envs per node and lead-time slot: the sum of the delays). */
 int imenv_state_layout(const ImEnv* env, int32_t* elem_bytes, int32_t* row_len, int32_t* ring_depth);
 

@@ -165,11 +165,11 @@ double exact_reciprocal(double x) {
   return 1.0 / x;
 }
 
-// Can every value held in the packed state (inventory, backlog, unfulfilled orders, shipments in
-// transit, demand / order history) be proven to fit int16? Backlog grows by at most one period's
-// demand per period when uncapped; a shipment is at most backlog + demand, plus the split's
+// Upper bound of every value held in the packed state (inventory, backlog, unfulfilled orders,
+// shipments in transit, demand / order history); all of them are >= 0. Backlog grows by at most one
+// period's demand per period when uncapped; a shipment is at most backlog + demand, plus the split's
 // overshoot of (children - 1) units (its inner loop does not re-check the remaining amount).
-bool state_fits_int16(const ImEnvSpec& s) {
+int64_t state_bound(const ImEnvSpec& s) {
   const int N = s.num_nodes;
   int64_t B = 0;
   auto upd = [&](int64_t v) { if (v > B) B = v; };
@@ -180,7 +180,7 @@ bool state_fits_int16(const ImEnvSpec& s) {
     const int64_t shipb = blb + dm + IMENV_MAX_CHILDREN;
     upd(shipb);
   }
-  return B <= 32767;
+  return B;
 }
 
 int validate_and_derive(const ImEnvSpec& s, SpecDev& d, int& maxc) {
@@ -274,10 +274,16 @@ int validate_and_derive(const ImEnvSpec& s, SpecDev& d, int& maxc) {
   } else if (s.demand_dist != IMENV_DEMAND_CUSTOM) {
     return fail(IMENV_E_INVALID, "Unrecognised, Distribution Not Implemented");
   }
-  d.st16 = state_fits_int16(s) ? 1 : 0;
+  // narrowest element type the bounds allow; IMENV_STATE_BYTES=2|4 forces a wider one (testing)
+  const int64_t bound = state_bound(s);
+  d.es = bound <= 255 ? 1 : (bound <= 32767 ? 2 : 4);
+  if (const char* v = std::getenv("IMENV_STATE_BYTES")) {
+    const int want = std::atoi(v);
+    if ((want == 2 || want == 4) && want > d.es) d.es = want;
+  }
   d.inv_bma = exact_reciprocal(s.b - s.a);
   d.inv_n = exact_reciprocal((double)N);
-  d.np = d.st16 ? ((N + 1) & ~1) : N;
+  d.np = d.es == 1 ? ((N + 3) & ~3) : (d.es == 2 ? ((N + 1) & ~1) : N);
   return IMENV_OK;
 }
 
@@ -303,7 +309,7 @@ struct ImEnv {
   int64_t n = 0;
   int64_t env_offset = 0;
   int maxc = 0;
-  size_t es = 4;       // state element size (2 or 4)
+  size_t es = 4;       // state element size (1, 2 or 4)
   void *d_inv = nullptr, *d_bl = nullptr, *d_ou = nullptr, *d_ring = nullptr, *d_hist_d = nullptr, *d_hist_o = nullptr;
   int32_t *d_carry = nullptr, *d_bto = nullptr, *d_demand = nullptr;
   double* d_delay_u = nullptr;
@@ -363,7 +369,7 @@ int imenv_create(const ImEnvSpec* spec, int64_t n_envs, int64_t env_offset, int 
   h->env_offset = env_offset;
   h->noisy_delay = spec->noisy_delay != 0;
   h->noisy_thr = spec->noisy_delay_threshold;
-  h->es = h->host.st16 ? 2 : 4;
+  h->es = (size_t)h->host.es;
   const ImEnvSpec& s = *spec;
   const size_t n = n_envs, np = h->host.np, rowb = n * np * h->es;
   bool uses_hist = false;
@@ -504,7 +510,7 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
   LaunchCfg c;
   c.mc = h->maxc;
   c.base = is_base_obs(s);
-  c.st16 = h->host.st16 != 0;
+  c.es = h->host.es;
   c.grid = (unsigned)((h->n + 255) / 256);
   c.stream = st;
   const int N = s.num_nodes;
@@ -544,8 +550,8 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
   }
   {
     char tag[96];
-    std::snprintf(tag, sizeof tag, "aot:imenv_step_kernel[NT=%d,MC=%d,base=%d,st16=%d]", N <= 8 ? N : 16, c.mc,
-                  c.base ? 1 : 0, c.st16 ? 1 : 0);
+    std::snprintf(tag, sizeof tag, "aot:imenv_step_kernel[NT=%d,MC=%d,base=%d,es=%d]", N <= 8 ? N : 16, c.mc,
+                  c.base ? 1 : 0, c.es);
     h->last_kernel = tag;
   }
   switch (N) {   // exact kernels for N <= 8, padded NT = 16 above
@@ -588,7 +594,10 @@ int imenv_get_state(ImEnv* h, int32_t* inv, int32_t* backlog, int32_t* order_u, 
     int32_t* dst[3] = {inv, backlog, order_u};
     for (int k = 0; k < 3; ++k) {
       if (!dst[k]) continue;
-      if (h->host.st16)
+      if (h->host.es == 1)
+        hipLaunchKernelGGL(imenv_unpack_kernel<uint8_t>, dim3(grid), dim3(256), 0, st,
+                           static_cast<const uint8_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes);
+      else if (h->host.es == 2)
         hipLaunchKernelGGL(imenv_unpack_kernel<int16_t>, dim3(grid), dim3(256), 0, st,
                            static_cast<const int16_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes);
       else

@@ -12,9 +12,9 @@
 //   JitSpec (generated)        every spec value is a constexpr: hipRTC compiles one kernel per
 //                              spec with all constants folded into immediates (imenv_jit.cpp)
 //
-// HBM layout. ST = int16 when the spec's bounds prove every value fits, else
-// int32. NP = row length in ST elements (N, rounded up to even for int16 so rows are
-// 4-byte aligned).
+// HBM layout. ST = uint8 / int16 when the spec's bounds prove every value fits
+// (0..255 / 32767), else int32. NP = row length in ST elements (N rounded up so rows are 4-byte
+// aligned: to a multiple of 4 for uint8, of 2 for int16).
 //   inv, backlog, order_u   [n][NP] ST      one packed row per env: 8 B per lane for N=4 int16
 //   ring (in transit)       [sum d_i][n] ST node-major, d_i slots per node: node i's slot
 //                                           (t mod d_i) holds what arrives at t (shipped at t - d_i)
@@ -36,6 +36,7 @@
 #include <cstdint>
 #else
 typedef signed char int8_t;
+typedef unsigned char uint8_t;
 typedef short int16_t;
 typedef unsigned short uint16_t;
 typedef int int32_t;
@@ -62,7 +63,7 @@ struct SpecDev {
   int32_t ring_off[IMENV_MAX_NODES];        // first ring row of node i (sum of earlier delays)
   int32_t ring_total;                       // ring rows = sum of delays
   int32_t np;                               // packed row length (elements)
-  int32_t st16;                             // state element type: 1 = int16, 0 = int32
+  int32_t es;                               // state element bytes: 1 (uint8), 2 (int16) or 4 (int32)
   int32_t table_len;
   uint32_t table[IMENV_TABLE_MAX];          // Poisson inversion thresholds
   // observation lookup: value of group g, node i for raw v in [0, lut_max] at lut[lut_off + v]
@@ -235,7 +236,8 @@ __device__ __forceinline__ void store_words(void* __restrict__ p, const uint32_t
 // deliver raw words; unpack() turns them into ints.
 template <typename ST, int NT, bool EXACT>
 struct Row {
-  static constexpr int NPT = (sizeof(ST) == 2) ? ((NT + 1) & ~1) : NT;
+  static constexpr int ES = (int)sizeof(ST);
+  static constexpr int NPT = ES == 1 ? ((NT + 3) & ~3) : (ES == 2 ? ((NT + 1) & ~1) : NT);
   static constexpr int BYTES = NPT * (int)sizeof(ST);
   static constexpr int WORDS = BYTES / 4;
 
@@ -249,7 +251,8 @@ struct Row {
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
         if (i < N) {
-          if constexpr (sizeof(ST) == 2) w[i >> 1] |= ((uint32_t)(uint16_t)base[e * np + i]) << ((i & 1) * 16);
+          if constexpr (ES == 1) w[i >> 2] |= ((uint32_t)(uint8_t)base[e * np + i]) << ((i & 3) * 8);
+          else if constexpr (ES == 2) w[i >> 1] |= ((uint32_t)(uint16_t)base[e * np + i]) << ((i & 1) * 16);
           else w[i] = (uint32_t)base[e * np + i];
         }
       }
@@ -259,7 +262,8 @@ struct Row {
   __device__ static __forceinline__ void unpack(const uint32_t (&w)[WORDS], int (&v)[NT]) {
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
-      if constexpr (sizeof(ST) == 2) v[i] = (int)(int16_t)((w[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu);
+      if constexpr (ES == 1) v[i] = (int)((w[i >> 2] >> ((i & 3) * 8)) & 0xFFu);   // values are >= 0
+      else if constexpr (ES == 2) v[i] = (int)(int16_t)((w[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu);
       else v[i] = (int)w[i];
     }
   }
@@ -279,7 +283,8 @@ struct Row {
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
         const int x = (i < N) ? v[i] : 0;
-        if constexpr (sizeof(ST) == 2) w[i >> 1] |= ((uint32_t)(uint16_t)(int16_t)x) << ((i & 1) * 16);
+        if constexpr (ES == 1) w[i >> 2] |= ((uint32_t)(uint8_t)x) << ((i & 3) * 8);
+        else if constexpr (ES == 2) w[i >> 1] |= ((uint32_t)(uint16_t)(int16_t)x) << ((i & 1) * 16);
         else w[i] = (uint32_t)x;
       }
       store_words<BYTES>(base + e * NPT, w);
@@ -881,7 +886,7 @@ __global__ void __launch_bounds__(P::BS) imenv_step_kernel(const SpecDev* __rest
 struct LaunchCfg {
   int mc;          // 0, 4, 8
   bool base;
-  bool st16;
+  int es;          // state element bytes 1 / 2 / 4
   unsigned grid;   // number of 256-env blocks
   hipStream_t stream;
 };

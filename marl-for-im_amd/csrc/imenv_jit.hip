@@ -152,7 +152,7 @@ std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f)
     << "  static constexpr bool JIT = true;\n"
     << "  static constexpr int TAB_LDS = " << (inline_tab ? 1 : IMENV_TABLE_MAX) << ";\n"
     << "  static constexpr int BS = " << jit_block_size() << ";\n"
-    << "  using ST = " << (d.st16 ? "int16_t" : "int32_t") << ";\n"
+    << "  using ST = " << (d.es == 1 ? "uint8_t" : d.es == 2 ? "int16_t" : "int32_t") << ";\n"
     << "  const imenv::SpecDev* __restrict__ sp;\n"
     << "  __device__ JitSpec(const imenv::SpecDev* __restrict__ s, const imenv::StepArgs&) : sp(s) {}\n";
   auto sc = [&](const char* type, const char* name, const std::string& v) {
@@ -333,8 +333,8 @@ bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const st
   out.fn = fn;
   out.bs = jit_block_size();
   char tag[160];
-  std::snprintf(tag, sizeof tag, "jit:imenv_step_jit[N=%d,MC=%d,base=%d,st16=%d,flags=0x%x,bs=%d,%zuB]",
-                d.s.num_nodes, maxc, base ? 1 : 0, d.st16, f.key(), out.bs, src.size());
+  std::snprintf(tag, sizeof tag, "jit:imenv_step_jit[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,%zuB]",
+                d.s.num_nodes, maxc, base ? 1 : 0, d.es, f.key(), out.bs, src.size());
   out.tag = tag;
   return true;
 }

@@ -11,13 +11,16 @@ void go(const LaunchCfg& c, const SpecDev* sp, const StepArgs& A) {
   hipLaunchKernelGGL((imenv_step_kernel<DynSpec<IMENV_NT, MC, BASE, ST>>), dim3(c.grid), dim3(256), 0, c.stream, sp,
                      A);
 }
+template <int MC, bool BASE>
+void go_st(const LaunchCfg& c, const SpecDev* sp, const StepArgs& A) {
+  if (c.es == 1) go<MC, BASE, uint8_t>(c, sp, A);
+  else if (c.es == 2) go<MC, BASE, int16_t>(c, sp, A);
+  else go<MC, BASE, int32_t>(c, sp, A);
+}
 template <int MC>
 void go_mc(const LaunchCfg& c, const SpecDev* sp, const StepArgs& A) {
-  if (c.base) {
-    if (c.st16) go<MC, true, int16_t>(c, sp, A); else go<MC, true, int32_t>(c, sp, A);
-  } else {
-    if (c.st16) go<MC, false, int16_t>(c, sp, A); else go<MC, false, int32_t>(c, sp, A);
-  }
+  if (c.base) go_st<MC, true>(c, sp, A);
+  else go_st<MC, false>(c, sp, A);
 }
 }  // namespace
 

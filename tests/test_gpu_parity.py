@@ -224,3 +224,33 @@ def test_gpu_errors_and_done():
         env.step(torch.zeros((64, 4), device=DEV))
     with pytest.raises(ImEnvNativeError):
         env.step(torch.zeros((64, 4), device=DEV))        # past the horizon (reference: IndexError)
+
+
+@pytest.mark.parametrize("name", ["C2_MAIM4", "C4_MAIM_div1", "IM4_td_pd_pa_L2", "MAIM_div2_share",
+                                  "IM4_noisy_delay"])
+@pytest.mark.parametrize("state_bytes", ["2", "4"])
+def test_gpu_wider_state_layouts_match_reference(name, state_bytes, monkeypatch):
+    """The packed state uses the narrowest element type the spec's bounds allow (uint8 for these
+    cases); forcing int16 / int32 rows must give the same bit-exact results."""
+    monkeypatch.setenv("IMENV_STATE_BYTES", state_bytes)
+    meta, d = load_case(name)
+    from imenv import VectorInvEnv
+    probe = VectorInvEnv(meta["kind"], meta["config"], n_envs=4, device=DEV)
+    assert probe.state_layout()[0] == int(state_bytes)
+    probe.close()
+    obs0, out, anyerr = run_gpu_case(meta, d)
+    assert anyerr == 0
+    for k in ("order", "demand", "acquisition", "ship", "inv", "backlog", "order_u", "profit", "obs"):
+        np.testing.assert_array_equal(out[k].astype(np.float64), d[k], err_msg="%s/%s" % (name, k))
+
+
+def test_gpu_narrowest_layout_selected():
+    from imenv import VectorInvEnv
+    meta, _ = load_case("C2_MAIM4")
+    env = VectorInvEnv(meta["kind"], meta["config"], n_envs=4, device=DEV)
+    assert env.state_layout()[0] == 1          # every C2 value is provably <= 255
+    env.close()
+    meta, _ = load_case("MAIM3_defaults")      # inv_max 200: shipments can exceed 255
+    env = VectorInvEnv(meta["kind"], meta["config"], n_envs=4, device=DEV)
+    assert env.state_layout()[0] == 2
+    env.close()
