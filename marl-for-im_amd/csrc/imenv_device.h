@@ -434,6 +434,10 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   const int np = p.np();
   const int t = A.t;
   const bool poisson = p.demand_layout() == IMENV_LAYOUT_DRAW && p.demand_dist() == IMENV_DEMAND_POISSON;
+  const uint32_t ep = *A.episode;   // scalar load issued first: the draws below need it
+  const uint32_t gid = A.env_offset + (uint32_t)e;
+  const uint64_t seed = p.seed();
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 
   ST* __restrict__ p_inv = static_cast<ST*>(A.inv);
   ST* __restrict__ p_bl = static_cast<ST*>(A.bl);
@@ -457,49 +461,88 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   for (int q = 0; q < R32::WORDS; ++q) w_cin[q] = w_bto[q] = 0;
 #pragma unroll
   for (int i = 0; i < NT; ++i) { cdem[i] = 0; du[i] = 1.0; r_arr[i] = 0; }
-  if (valid) {
+  {
+    // every lane loads (a tail lane re-reads the last env; only stores are guarded): no branch, so the
+    // loads and the draws below share one basic block and the draws run under the loads' latency
+    const int64_t el = valid ? e : n - 1;
     if (EXACT) {
       if (p.act_f64()) {
-        load_words<8 * NT>(static_cast<const double*>(A.actions) + e * NT, aw);
+        load_words<8 * NT>(static_cast<const double*>(A.actions) + el * NT, aw);
       } else {
         uint32_t (&a32)[NT] = *reinterpret_cast<uint32_t(*)[NT]>(aw);
-        load_words<4 * NT>(static_cast<const float*>(A.actions) + e * NT, a32);
+        load_words<4 * NT>(static_cast<const float*>(A.actions) + el * NT, a32);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
         if (i < N) {
           if (p.act_f64()) {
-            const uint2 v = reinterpret_cast<const uint2*>(static_cast<const double*>(A.actions) + e * N)[i];
+            const uint2 v = reinterpret_cast<const uint2*>(static_cast<const double*>(A.actions) + el * N)[i];
             aw[2 * i] = v.x; aw[2 * i + 1] = v.y;
           } else {
-            aw[i] = reinterpret_cast<const uint32_t*>(static_cast<const float*>(A.actions) + e * N)[i];
+            aw[i] = reinterpret_cast<const uint32_t*>(static_cast<const float*>(A.actions) + el * N)[i];
           }
         }
       }
     }
     // state and arrivals are loaded even at t == 0 (then ignored): unconditional, branch-free loads
-    R::load(p_inv, e, np, N, w_inv);
-    R::load(p_bl, e, np, N, w_bl);
-    R::load(p_ou, e, np, N, w_ou);
+    R::load(p_inv, el, np, N, w_inv);
+    R::load(p_bl, el, np, N, w_bl);
+    R::load(p_ou, el, np, N, w_ou);
 #pragma unroll
     for (int i = 0; i < NT; ++i)
-      if (i < N) r_arr[i] = p_ring[(int64_t)A.ring_row[i] * n + e];
-    if (p.noisy_delay()) R32::load(p_carry, e, np, N, w_cin);
-    if (MC > 0) R32::load(p_bto, e, np, N, w_bto);
+      if (i < N) r_arr[i] = p_ring[(int64_t)A.ring_row[i] * n + el];
+    if (p.noisy_delay()) R32::load(p_carry, el, np, N, w_cin);
+    if (MC > 0) R32::load(p_bto, el, np, N, w_bto);
     if (p.demand_layout() == IMENV_LAYOUT_PER_ENV) {
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
         const int r = (i < N) ? p.retailer_slot(i) : -1;
-        if (r >= 0) cdem[i] = A.demand[((int64_t)t * p.num_retailers() + r) * n + e];
+        if (r >= 0) cdem[i] = A.demand[((int64_t)t * p.num_retailers() + r) * n + el];
       }
     }
     if (p.has_delay_u()) {
 #pragma unroll
-      for (int i = 0; i < NT; ++i) if (i < N) du[i] = A.delay_u[((int64_t)t * N + i) * n + e];
+      for (int i = 0; i < NT; ++i) if (i < N) du[i] = A.delay_u[((int64_t)t * N + i) * n + el];
     }
   }
   p.stage_tables(s_tab, poisson);
+
+  // (A2) random draws depend on no loaded value: placed before the first use of a load, they
+  // execute under the loads' latency instead of after the wait
+  int cdraw[NT];
+  bool nd_double[NT], nd_zero[NT], nd_delay[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    cdraw[i] = 0;
+    nd_double[i] = nd_zero[i] = nd_delay[i] = false;
+    if (i < N) {
+      const int r = p.retailer_slot(i);
+      if (r >= 0) {
+        if (p.demand_layout() == IMENV_LAYOUT_DRAW) {
+          const uint32_t w = philox_word(gid, ep, (uint32_t)t, (STREAM_DEMAND << 16) | (uint32_t)(r >> 2), k0, k1,
+                                         r & 3);
+          if (poisson) {
+            cdraw[i] = p.poisson_draw(w, s_tab);
+          } else {
+            const uint64_t rng = (uint64_t)(p.uniform_high() - p.uniform_low());
+            cdraw[i] = p.uniform_low() + (int)(((uint64_t)w * rng) >> 32);
+          }
+        }
+        if (p.noisy_demand()) {
+          const uint32_t wd = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_DOUBLE << 16) | (uint32_t)(r >> 2), k0, k1,
+                                          r & 3);
+          const uint32_t wz = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_ZERO << 16) | (uint32_t)(r >> 2), k0, k1,
+                                          r & 3);
+          nd_double[i] = (uint64_t)wd < A.noisy_demand_thr32;
+          nd_zero[i] = (uint64_t)wz < A.noisy_demand_thr32;
+        }
+      }
+      if (p.noisy_delay() && !p.has_delay_u() && t >= p.delay(i))
+        nd_delay[i] = (uint64_t)philox_word(gid, ep, (uint32_t)t, (STREAM_NOISY_DELAY << 16) | (uint32_t)(i >> 2), k0,
+                                            k1, i & 3) < A.noisy_delay_thr32;
+    }
+  }
 
   // unpack (first use of the loaded words)
   double x[NT];
@@ -526,10 +569,6 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   }
 
   // ================= (B) compute
-  const uint32_t ep = *A.episode;
-  const uint32_t gid = A.env_offset + (uint32_t)e;
-  const uint64_t seed = p.seed();
-  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const double a = p.a();
   const double bma = p.bma();
   int order[NT], dem[NT], acq[NT], ship[NT], sto[NT], cout[NT], push[NT];
@@ -563,22 +602,11 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
         } else if (p.demand_layout() == IMENV_LAYOUT_BROADCAST) {
           cd = A.demand[t * p.num_retailers() + r];
         } else {
-          const uint32_t w = philox_word(gid, ep, (uint32_t)t, (STREAM_DEMAND << 16) | (uint32_t)(r >> 2), k0, k1,
-                                         r & 3);
-          if (poisson) {
-            cd = p.poisson_draw(w, s_tab);
-          } else {
-            const uint64_t rng = (uint64_t)(p.uniform_high() - p.uniform_low());
-            cd = p.uniform_low() + (int)(((uint64_t)w * rng) >> 32);
-          }
+          cd = cdraw[i];
         }
-        if (p.noisy_demand()) {
-          const uint32_t wd = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_DOUBLE << 16) | (uint32_t)(r >> 2), k0, k1,
-                                          r & 3);
-          const uint32_t wz = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_ZERO << 16) | (uint32_t)(r >> 2), k0, k1,
-                                          r & 3);
-          if ((uint64_t)wd < A.noisy_demand_thr32) cd = 2 * cd;
-          if ((uint64_t)wz < A.noisy_demand_thr32) cd = 0;
+        if (p.noisy_demand()) {   // IM_div_env.py:246-255: double, then zero
+          if (nd_double[i]) cd = 2 * cd;
+          if (nd_zero[i]) cd = 0;
         }
         dem[i] = min(cd, p.inv_max(i));
       } else {
@@ -599,8 +627,7 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
       if (p.noisy_delay() && t >= p.delay(i)) {
         bool extra;
         if (p.has_delay_u()) extra = du[i] <= A.noisy_delay_thr;
-        else extra = (uint64_t)philox_word(gid, ep, (uint32_t)t, (STREAM_NOISY_DELAY << 16) | (uint32_t)(i >> 2),
-                                           k0, k1, i & 3) < A.noisy_delay_thr32;
+        else extra = nd_delay[i];
         if (extra && t < T - 1) { cout[i] = q; q = 0; }
       }
       acq[i] = q;
