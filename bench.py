@@ -110,12 +110,13 @@ def _cpu_baseline_here(seconds):
 # ----------------------------------------------------------------- PMC traffic
 def pmc_traffic(n_envs, kernel):
     """HBM bytes per step-kernel launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_step_kernel.json, written by tools/pmc_summary.py for this workload), else None."""
+    (profiles/pmc_step_kernel.json, written by tools/profile_pmc.sh -> tools/pmc_summary.py for
+    this workload), else None. Only a summary of this exact kernel variant (kernel_info) counts."""
     p = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if int(d.get("n_envs", -1)) == int(n_envs) and d.get("kernel", "?") in kernel:
+        if int(d.get("n_envs", -1)) == int(n_envs) and d.get("kernel_info") == kernel:
             return float(d["hbm_bytes_per_launch"])
     except Exception:
         pass
@@ -257,7 +258,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "%s state, f64 reward, f32 obs/actions" % ("int16" if es == 2 else "int32"),
+        "dtype": "%s state, f64 reward, f32 obs/actions" % {1: "u8", 2: "int16", 4: "int32"}[es],
         "data": "synthetic: in-kernel Philox4x32-10 Poisson(5) demand, uniform[-1,1] f32 actions (torch seed 0)",
         "config": {
             "workload": "C2 shape at the metric's size: MultiAgentInvManagement 4-stage serial "

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc CSVs: per-kernel mean counter values per dispatch.
 
-    python tools/pmc_summary.py OUT.json N_ENVS DIR [DIR ...]
+    python tools/pmc_summary.py OUT.json N_ENVS DIR [DIR ...] [--bench-log LOG]
 
 Each DIR is one rocprofv3 -d output (one --pmc pass). Kernel names are shortened
 to their template head. If the calibration kernels (tools/pmc_calib.hip, 1 GiB per
@@ -48,10 +48,25 @@ def load(dirs):
 
 
 def main():
-    outp = sys.argv[1]
-    n_envs = int(sys.argv[2])
-    s = load(sys.argv[3:])
+    argv = sys.argv[1:]
+    bench = None
+    if "--bench-log" in argv:
+        i = argv.index("--bench-log")
+        bench = argv[i + 1]
+        del argv[i:i + 2]
+    outp = argv[0]
+    n_envs = int(argv[1])
+    s = load(argv[2:])
     res = {"kernels": s, "n_envs": n_envs}
+    if bench:
+        # the bench line of the profiled run names the exact kernel variant (bench.py only trusts a
+        # PMC summary whose kernel_info equals the kernel it is timing)
+        for line in open(bench):
+            line = line.strip()
+            if line.startswith("{") and '"roofline"' in line:
+                rl = json.loads(line)["roofline"]
+                res["kernel_info"] = rl["kernel"]
+                res["algorithmic_bytes_per_launch"] = rl["bytes_per_launch"]
     fac = {}
     for k, c in (("read_dword", "FETCH_SIZE"), ("read_dwordx4", "FETCH_SIZE"), ("write_dword", "WRITE_SIZE"),
                  ("write_dwordx4", "WRITE_SIZE")):

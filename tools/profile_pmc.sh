@@ -13,5 +13,5 @@ CMD=$BENCH; run fetch FETCH_SIZE; run write WRITE_SIZE
 run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
 run tcc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE
 run sq2 SQ_LEVEL_WAVES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_FLAT || echo "sq2 pass failed (counter names?)"
-python tools/pmc_summary.py $OUT/summary.json 1048576 $OUT/cal_fetch $OUT/cal_write $OUT/fetch $OUT/write $OUT/sq $OUT/tcc $OUT/sq2 > $OUT/summary.log 2>&1
+python tools/pmc_summary.py $OUT/summary.json 1048576 $OUT/cal_fetch $OUT/cal_write $OUT/fetch $OUT/write $OUT/sq $OUT/tcc $OUT/sq2 --bench-log $OUT/fetch.log > $OUT/summary.log 2>&1
 echo "pmc passes done"
