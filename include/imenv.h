@@ -182,6 +182,39 @@ typedef struct ImEnvInfo {
   int32_t* backlog_to;   /* backlog_to[parent][c] after the step (0 unless parent splits) */
 } ImEnvInfo;
 
+/* Per-episode metrics of a fused base-stock rollout (imenv_base_stock_rollout) */
+#define IMENV_STAT_RETURN 0            /* sum_t reward (eval loop, inv_management.py:222-232) */
+#define IMENV_STAT_OBJECTIVE 1         /* dfo_func: -1/T * np.sum(pmf(customer_demand) * rewards)
+                                        * (base_restock_policy.py:24-45) */
+#define IMENV_STAT_INVENTORY 2         /* sum_t sum_i inventory after the step (inv_management.py:589-591) */
+#define IMENV_STAT_BACKLOG 3           /* sum_t sum_i backlog after the step */
+#define IMENV_STAT_CUSTOMER_BACKLOG 4  /* sum_t backlog of the retailers (inv_management.py:592: bl[0]) */
+#define IMENV_NUM_STATS 5
+
+/* Batched episodes of the order-up-to policy (base_restock_policy.py:4-21) run entirely on the
+ * device: num_policies x num_scenarios independent episodes of num_periods steps, each reset to
+ * period 0 and stepped with actions = min(order_max, max(policy - (inv + order_u - backlog), 0)).
+ * All pointers are device pointers. */
+typedef struct ImEnvRollout {
+  const double* policy;       /* [P][N] order-up-to level per node (float64, finite) */
+  int64_t num_policies;       /* P >= 1 */
+  int64_t num_scenarios;      /* S >= 1: demand scenarios (episodes) per policy */
+  /* customer demand int32 [T][R][S] (reset(customer_demand=...) per scenario, the same table for
+   * every policy), or NULL: drawn in-kernel per spec.demand_dist (+ noisy demand), Philox keyed by
+   * (spec.seed, scenario_offset + s, episode) exactly like imenv_reset's draws for env id s */
+  const int32_t* demand;
+  int64_t scenario_offset;
+  int64_t episode;            /* Philox counter word (>= 0) */
+  /* dfo_func weights: demand_pmf[k] = env.dist.pmf(k) for k < pmf_len (values outside -> 0).
+   * NULL: no objective (IMENV_STAT_OBJECTIVE reads 0). Needs num_retailers * T <= 128. */
+  const double* demand_pmf;
+  int32_t pmf_len;
+  int32_t noisy_delay;        /* reset(noisy_delay=True, noisy_delay_threshold) (IM_env.py:180-182) */
+  double noisy_delay_threshold;
+  double* episode_stats;      /* out [IMENV_NUM_STATS][P][S], or NULL */
+  double* policy_stats;       /* out [P][IMENV_NUM_STATS][2]: np.mean, np.std over the S episodes, or NULL */
+} ImEnvRollout;
+
 /* Replaces the constructors: InvManagement.__init__ (IM_env.py:7-162),
  * MultiAgentInvManagement.__init__ (MAIM_env.py:8-173), InvManagementDiv.__init__
  * (IM_div_env.py:9-199), MultiAgentInvManagementDiv.__init__ (MAIM_div_env.py:9-237).
@@ -211,6 +244,14 @@ int imenv_reset(ImEnv* env, const int32_t* demand, int demand_layout, int noisy_
  * info: optional. done_out (HOST int*, may be NULL) receives period >= T. */
 int imenv_step(ImEnv* env, const void* actions, int action_dtype, void* obs, int obs_dtype,
                double* reward, const ImEnvInfo* info, int32_t* done_out, void* stream);
+
+/* Replaces dfo_func(policy, env, demand) (base_restock_policy.py:24-45) and the base-stock
+ * evaluation loop (inv_management.py:222-232) for many policies and scenarios at once: one fused
+ * launch (state in registers, lead-time queue in LDS, wavefront reductions of the metrics) plus a
+ * small deterministic reduction launch for policy_stats. Scalar-reward specs only (IMENV_REWARD_SUM /
+ * SHARED_MEAN). Independent of the handle's own env state (it may be mid-episode); uses its spec,
+ * device and kernel cache. Always runs a hipRTC-specialised kernel (IMENV_E_UNSUPPORTED without it). */
+int imenv_base_stock_rollout(ImEnv* env, const ImEnvRollout* args, void* stream);
 
 /* State the reference's callers read directly (base_restock_policy.py:12:
  * env.inv/order_u/backlog[env.period]). Copies int32 [N][n] SoA into the given
@@ -257,7 +298,9 @@ int imenv_kernel_info(const ImEnv* env, char* buf, int64_t len);
 
 /* Diagnostics (no device needed): generate and compile with hipRTC the specialised step kernel of
  * `spec` for `arch` (e.g. "gfx950"); flags = bit0 f64 actions, bit1 f64 obs, bit2 noisy delay,
- * bit3 noisy demand, bit4 host-fed delay uniforms, bits 5+ demand layout. `log` receives "ok" or
+ * bit3 noisy demand, bit4 host-fed delay uniforms, bits 5-11 demand layout. With bit 12 set it
+ * compiles the base-stock rollout kernel instead: bit13 demand table, bit14 noisy delay, bit15 noisy
+ * demand, bit16 objective, bit17 objective terms in LDS (> 1 retailer). `log` receives "ok" or
  * the compiler log. */
 int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, char* log, int64_t log_len);
 

@@ -65,6 +65,44 @@ __global__ void __launch_bounds__(256) imenv_unpack_kernel(const ST* __restrict_
   for (int i = 0; i < N; ++i) dst[i * n + e] = (int32_t)src[e * np + i];
 }
 
+// policy_stats of a base-stock rollout: one block per policy and metric. np.mean over the S
+// episodes from the rollout kernel's per-block partial sums, then np.std's second pass over the
+// per-episode values: mean(|x - mean|^2). Strided per-thread sums, wavefront shuffles and a fixed
+// wave order through LDS: deterministic, the same bits for the same inputs.
+__global__ void __launch_bounds__(256) imenv_rollout_stats_kernel(const double* __restrict__ ep,
+                                                                  const double* __restrict__ partial,
+                                                                  double* __restrict__ out, int64_t P, int64_t S,
+                                                                  int64_t bpp) {
+  __shared__ double s_w[4];
+  __shared__ double s_mean;
+  const int64_t pol = blockIdx.x;
+  const int m = blockIdx.y;
+  const int tid = threadIdx.x;
+  auto block_sum = [&](double v) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((tid & 63) == 0) s_w[tid >> 6] = v;
+    __syncthreads();
+    const double r = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);
+    __syncthreads();
+    return r;
+  };
+  double a = 0.0;
+  for (int64_t k = tid; k < bpp; k += 256) a += partial[((int64_t)m * P + pol) * bpp + k];
+  const double mean = block_sum(a) / (double)S;
+  if (tid == 0) s_mean = mean;
+  const double* x = ep + ((int64_t)m * P + pol) * S;
+  double q = 0.0;
+  for (int64_t k = tid; k < S; k += 256) {
+    const double d = x[k] - mean;
+    q += d * d;
+  }
+  const double var = block_sum(q) / (double)S;
+  if (tid == 0) {
+    out[(pol * IMENV_NUM_STATS + m) * 2 + 0] = s_mean;
+    out[(pol * IMENV_NUM_STATS + m) * 2 + 1] = sqrt(var);
+  }
+}
+
 thread_local std::string g_err;
 
 int fail(int code, const std::string& msg) {
@@ -333,6 +371,13 @@ struct ImEnv {
   std::unordered_map<uint32_t, imenv::JitKernel> jit_k;
   std::string jit_err;
   std::string last_kernel;
+  // base-stock rollout: kernels per RolloutFlags, scratch for per-episode metrics and block sums
+  std::unordered_map<uint32_t, imenv::JitKernel> roll_k;
+  double* d_roll_ep = nullptr;
+  size_t roll_ep_cap = 0;
+  double* d_roll_part = nullptr;
+  size_t roll_part_cap = 0;
+  std::string last_rollout;
 };
 
 extern "C" {
@@ -348,10 +393,12 @@ void imenv_destroy(ImEnv* h) {
   (void)hipSetDevice(h->device);
   void* ptrs[] = {h->d_spec, h->d_inv, h->d_bl, h->d_ou, h->d_ring, h->d_carry, h->d_bto, h->d_hist_d,
                   h->d_hist_o, h->d_demand, h->d_delay_u, h->d_err, h->d_err_any, h->d_lut32, h->d_lut64,
-                  h->d_episode};
+                  h->d_episode, h->d_roll_ep, h->d_roll_part};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& kv : h->jit_k)
+    if (kv.second.mod) (void)hipModuleUnload(kv.second.mod);
+  for (auto& kv : h->roll_k)
     if (kv.second.mod) (void)hipModuleUnload(kv.second.mod);
   delete h;
 }
@@ -571,6 +618,90 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
   return IMENV_OK;
 }
 
+int imenv_base_stock_rollout(ImEnv* h, const ImEnvRollout* r, void* stream) {
+  if (!h || !r || !r->policy) return fail(IMENV_E_INVALID, "null argument");
+  const ImEnvSpec& s = h->host.s;
+  if (s.reward_mode == IMENV_REWARD_INDEPENDENT)
+    return fail(IMENV_E_UNSUPPORTED, "base-stock rollout needs a scalar reward (independent multi-agent rewards)");
+  if (r->num_policies < 1 || r->num_scenarios < 1) return fail(IMENV_E_INVALID, "num_policies / num_scenarios < 1");
+  if (r->scenario_offset < 0 || r->scenario_offset + r->num_scenarios > (int64_t(1) << 32))
+    return fail(IMENV_E_INVALID, "scenario ids must fit 32 bits");
+  if (r->episode < 0 || r->episode > 0xFFFFFFFFll) return fail(IMENV_E_INVALID, "episode must fit 32 bits");
+  if (!r->demand && s.demand_dist != IMENV_DEMAND_POISSON && s.demand_dist != IMENV_DEMAND_UNIFORM)
+    return fail(IMENV_E_INVALID, "custom demand needs a table");
+  if (r->demand_pmf && (r->pmf_len < 1 || (int64_t)s.num_retailers * s.num_periods > 128))
+    return fail(r->pmf_len < 1 ? IMENV_E_INVALID : IMENV_E_UNSUPPORTED,
+                "objective: pmf_len >= 1 and num_retailers * num_periods <= 128 (np.sum without recursion)");
+  if (h->arch.empty()) return fail(IMENV_E_UNSUPPORTED, "base-stock rollout needs hipRTC (device arch unknown)");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  HIPCHK(hipSetDevice(h->device));
+  imenv::RolloutFlags f;
+  f.table = r->demand != nullptr;
+  f.noisy_delay = r->noisy_delay != 0;
+  f.noisy_demand = !f.table && s.noisy_demand != 0;
+  f.objective = r->demand_pmf != nullptr;
+  f.lds_terms = f.objective && s.num_retailers > 1;
+  auto it = h->roll_k.find(f.key());
+  if (it == h->roll_k.end()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs);
+    if (cs != hipStreamCaptureStatusNone)
+      return fail(IMENV_E_UNSUPPORTED, "first rollout of a flag combination cannot be captured (it compiles)");
+    imenv::JitKernel k;
+    std::string msg;
+    if (!imenv::jit_rollout_load(h->host, h->maxc, f, h->arch, k, msg))
+      return fail(IMENV_E_UNSUPPORTED, "rollout kernel: " + msg);
+    it = h->roll_k.emplace(f.key(), k).first;
+  }
+  const imenv::JitKernel& k = it->second;
+  const int64_t P = r->num_policies, S = r->num_scenarios;
+  const int64_t bpp = (S + k.bs - 1) / k.bs;
+  if (P * bpp > 0x7FFFFFFFll) return fail(IMENV_E_INVALID, "num_policies * ceil(num_scenarios / block) too large");
+  double* ep = r->episode_stats;
+  if (!ep) {
+    const size_t need = (size_t)IMENV_NUM_STATS * P * S;
+    if (h->roll_ep_cap < need) {
+      if (h->d_roll_ep) { HIPCHK(hipStreamSynchronize(st)); HIPCHK(hipFree(h->d_roll_ep)); h->d_roll_ep = nullptr; }
+      int rc = alloc(&h->d_roll_ep, need);
+      if (rc) return rc;
+      h->roll_ep_cap = need;
+    }
+    ep = h->d_roll_ep;
+  }
+  const size_t pneed = (size_t)IMENV_NUM_STATS * P * bpp;
+  if (h->roll_part_cap < pneed) {
+    if (h->d_roll_part) { HIPCHK(hipStreamSynchronize(st)); HIPCHK(hipFree(h->d_roll_part)); h->d_roll_part = nullptr; }
+    int rc = alloc(&h->d_roll_part, pneed);
+    if (rc) return rc;
+    h->roll_part_cap = pneed;
+  }
+  imenv::RolloutArgs A;
+  std::memset(&A, 0, sizeof(A));
+  A.policy = r->policy;
+  A.demand = r->demand;
+  A.pmf = r->demand_pmf;
+  A.pmf_len = r->demand_pmf ? r->pmf_len : 0;
+  A.ep = ep;
+  A.partial = h->d_roll_part;
+  A.S = S;
+  A.P = P;
+  A.bpp = bpp;
+  A.scen_offset = (uint32_t)r->scenario_offset;
+  A.episode = (uint32_t)r->episode;
+  A.noisy_delay = f.noisy_delay ? 1 : 0;
+  A.noisy_demand = f.noisy_demand ? 1 : 0;
+  A.noisy_delay_thr32 = prob_thr32(r->noisy_delay_threshold);
+  A.noisy_demand_thr32 = prob_thr32(s.noisy_demand_threshold);
+  HIPCHK(imenv::jit_rollout_launch(k, st, h->d_spec, A));
+  h->last_rollout = k.tag;
+  if (r->policy_stats) {
+    hipLaunchKernelGGL(imenv_rollout_stats_kernel, dim3((unsigned)P, IMENV_NUM_STATS), dim3(256), 0, st, ep,
+                       h->d_roll_part, r->policy_stats, P, S, bpp);
+    HIPCHK(hipGetLastError());
+  }
+  return IMENV_OK;
+}
+
 int imenv_get_state(ImEnv* h, int32_t* inv, int32_t* backlog, int32_t* order_u, int32_t* period, void* stream) {
   if (!h) return fail(IMENV_E_INVALID, "null handle");
   const ImEnvSpec& s = h->host.s;
@@ -691,6 +822,7 @@ int imenv_kernel_info(const ImEnv* h, char* buf, int64_t len) {
   std::string s = h->last_kernel.empty() ? std::string(h->jit ? "jit (no step yet)" : "aot (no step yet)")
                                          : h->last_kernel;
   if (!h->jit_err.empty()) s += " | jit failed: " + h->jit_err;
+  if (!h->last_rollout.empty()) s += " | rollout " + h->last_rollout;
   std::snprintf(buf, (size_t)len, "%s", s.c_str());
   return IMENV_OK;
 }
@@ -713,7 +845,22 @@ int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, cha
   f.has_delay_u = flags & 16u;
   f.demand_layout = (int)(flags >> 5);
   std::string msg;
-  auto code = imenv::jit_compile(imenv::jit_source(d, maxc, is_base_obs(*spec), f), arch, msg);
+  std::string src;
+  if (flags & (1u << 12)) {   // the base-stock rollout kernel; bits 13..17 = RolloutFlags::key()
+    imenv::RolloutFlags rf;
+    const uint32_t rk = flags >> 13;
+    rf.table = rk & 1u;
+    rf.noisy_delay = rk & 2u;
+    rf.noisy_demand = rk & 4u;
+    rf.objective = rk & 8u;
+    rf.lds_terms = rk & 16u;
+    const int bs = imenv::rollout_block_size(d, rf);
+    if (bs == 0) return fail(IMENV_E_UNSUPPORTED, "rollout does not fit LDS");
+    src = imenv::jit_rollout_source(d, maxc, rf, bs);
+  } else {
+    src = imenv::jit_source(d, maxc, is_base_obs(*spec), f);
+  }
+  auto code = imenv::jit_compile(src, arch, msg);
   if (log && log_len > 0) std::snprintf(log, (size_t)log_len, "%s", code ? "ok" : msg.c_str());
   if (!code) return fail(IMENV_E_UNSUPPORTED, "hipRTC: " + msg);
   return IMENV_OK;

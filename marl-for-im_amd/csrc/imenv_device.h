@@ -116,6 +116,27 @@ struct StepArgs {
   int32_t ring_row[IMENV_MAX_NODES];  // ring_off[i] + t mod delay[i]
 };
 
+// Fused base-stock rollout (imenv_base_stock_rollout): whole episodes of P policies x S demand
+// scenarios in one launch, state in registers, the in-transit queue in LDS.
+struct RolloutArgs {
+  const double* policy;       // [P][N] order-up-to levels
+  const int32_t* demand;      // [T][R][S] customer demand per scenario, or null: drawn in-kernel
+  const double* pmf;          // [pmf_len] dfo_func weight of a customer-demand value (objective only)
+  double* ep;                 // [IMENV_NUM_STATS][P][S] per-episode metrics
+  double* partial;            // [IMENV_NUM_STATS][P][bpp] per-block sums (wavefront reductions)
+  int64_t S;                  // scenarios per policy
+  int64_t P;                  // policies
+  int64_t bpp;                // blocks per policy = ceil(S / BS)
+  uint32_t scen_offset;       // global id of scenario 0 (Philox key, sharding)
+  uint32_t episode;           // Philox counter word
+  int32_t pmf_len;
+  int32_t noisy_delay;
+  int32_t noisy_demand;
+  int32_t pad_;
+  uint64_t noisy_delay_thr32;
+  uint64_t noisy_demand_thr32;
+};
+
 constexpr uint32_t PH_M0 = 0xD2511F53u, PH_M1 = 0xCD9E8D57u;
 constexpr uint32_t PH_W0 = 0x9E3779B9u, PH_W1 = 0xBB67AE85u;
 constexpr uint32_t STREAM_DEMAND = 0, STREAM_ND_DOUBLE = 1, STREAM_ND_ZERO = 2, STREAM_NOISY_DELAY = 3;
@@ -410,6 +431,185 @@ __device__ __forceinline__ double DynSpec<NT_, MC_, BASE_, ST_>::obs64(int g, in
   return obs_value64(*this, lut, g, i, v);
 }
 
+// ---------------------------------------------------------------- one period of one env
+// The arithmetic of step() on register state (IM_env.py:287-374 and siblings): order decode,
+// demand, arrivals (noisy-delay deferral decided by the caller), shipment, divergent split,
+// balance equations, profit and reward. inv / bl / ou / btoc are updated in place. Shared by the
+// step kernel (state in HBM rows) and the fused rollout kernel (state in registers, in-transit
+// queue in LDS), so both compute one function.
+template <class P>
+__device__ __forceinline__ void step_core(const P& p, const int t, const double (&x)[P::NT], const int (&cust)[P::NT],
+                                          const bool (&defer)[P::NT], const int (&arr)[P::NT],
+                                          const int (&cin)[P::NT], int (&inv)[P::NT], int (&bl)[P::NT],
+                                          int (&ou)[P::NT], int (&btoc)[P::NT], int (&order)[P::NT],
+                                          int (&dem)[P::NT], int (&acq)[P::NT], int (&ship)[P::NT],
+                                          int (&sto)[P::NT], int (&cout)[P::NT], int (&push)[P::NT],
+                                          double (&prof)[P::NT], double& rew, bool& split_ok) {
+  constexpr int NT = P::NT;
+  constexpr int MC = P::MC;
+  const int N = p.N();
+  const int T = p.T();
+  const double a = p.a();
+  const double bma = p.bma();
+  // order decode (IM_env.py:298-302; MAIM_env.py:340-347). Division by b - a is replaced by
+  // an exact multiply when b - a is a power of two (inv_bma != 0).
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    order[i] = 0;
+    if (i < N) {
+      const double om = (double)p.order_max(i);
+      double v = x[i];
+      if (p.std_actions()) {
+        const double q = (x[i] - a) * (om - 0.0);
+        v = (p.inv_bma() != 0.0 ? q * p.inv_bma() : q / bma) + 0.0;
+      }
+      const double o = p.clip_round() ? rint(fmin(fmax(v, 0.0), om)) : fmin(fmax(rint(v), 0.0), om);
+      order[i] = (int)o;
+    }
+  }
+  // demand (IM_env.py:306-308, IM_div_env.py:380-387)
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    dem[i] = 0;
+    if (i < N) {
+      const int r = p.retailer_slot(i);
+      if (r >= 0) {
+        dem[i] = min(cust[i], p.inv_max(i));
+      } else {
+        int s = 0;
+#pragma unroll
+        for (int c = 0; c < NT; ++c)
+          if (c < N && p.demand_parent(c) == i) s += order[c];
+        dem[i] = s;
+      }
+    }
+  }
+  // arrivals (IM_env.py:376-414); noisy delay defers the whole arrival (plus any carried amount)
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    acq[i] = ship[i] = cout[i] = 0;
+    if (i < N) {
+      int q = arr[i] + cin[i];
+      if (defer[i] && t < T - 1) { cout[i] = q; q = 0; }
+      acq[i] = q;
+      ship[i] = min(bl[i] + dem[i], inv[i] + acq[i]);   // IM_env.py:315
+    }
+  }
+  // shipments into each node: a single-child parent's whole shipment, else the split
+#pragma unroll
+  for (int c = 0; c < NT; ++c) {
+    sto[c] = 0;
+    if (c < N) {
+      const int par = p.single_parent(c);
+      if (par >= 0) sto[c] = sel<NT>(ship, par);
+    }
+  }
+  split_ok = true;
+  if constexpr (MC > 0) {
+#pragma unroll
+    for (int si = 0; si < NT; ++si) {
+      if (si >= p.num_split()) break;
+      const int q = p.split_node(si);
+      const int m = p.num_children(q);
+      const int shp = sel<NT>(ship, q), dmp = sel<NT>(dem, q), blp = sel<NT>(bl, q);
+      int bto[MC], oc[MC], s[MC];
+#pragma unroll
+      for (int k = 0; k < MC; ++k) {
+        s[k] = 0; bto[k] = 0; oc[k] = 0;
+        if (k < m) {
+          const int c = p.child(q, k);
+          oc[k] = sel<NT>(order, c);
+          bto[k] = sel<NT>(btoc, c);
+        }
+      }
+      int amt = shp;
+      bool ok = true;
+      if (shp >= dmp) {
+        if (blp > 0) {        // backlog first, then outstanding orders (IM_div_env.py:409-454)
+          ok = rr_closed<MC, true>(m, bto, s, amt, p.split_limit(q, 0));
+          if (ok && amt > 0 && dmp > 0) {
+            int out[MC];
+#pragma unroll
+            for (int k = 0; k < MC; ++k) out[k] = oc[k];
+            ok = rr_closed<MC, true>(m, out, s, amt, p.split_limit(q, 1));
+#pragma unroll
+            for (int k = 0; k < MC; ++k) bto[k] += out[k];
+          }
+        } else {              // IM_div_env.py:457-460
+#pragma unroll
+          for (int k = 0; k < MC; ++k) s[k] += oc[k];
+        }
+      } else {
+        if (blp > 0) {        // IM_div_env.py:468-484
+          ok = rr_closed<MC, true>(m, bto, s, amt, p.split_limit(q, 2));
+        } else {              // IM_div_env.py:486-498: cap at order + backlog_to
+          int cap[MC];
+#pragma unroll
+          for (int k = 0; k < MC; ++k) cap[k] = oc[k] + bto[k];
+          ok = rr_closed<MC, false>(m, cap, s, amt, p.split_limit(q, 3));
+        }
+#pragma unroll
+        for (int k = 0; k < MC; ++k) bto[k] += oc[k] - s[k];   // IM_div_env.py:501-502
+      }
+      split_ok = split_ok && ok;
+#pragma unroll
+      for (int k = 0; k < MC; ++k) {
+        if (k < m) {
+          const int c = p.child(q, k);
+#pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            sto[j] = (c == j) ? s[k] : sto[j];
+            btoc[j] = (c == j) ? bto[k] : btoc[j];
+          }
+        }
+      }
+    }
+  }
+  // balance equations and profit (IM_env.py:318-340, 362-367)
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    prof[i] = 0.0;
+    push[i] = 0;
+    if (i < N) {
+      int b2 = bl[i] + dem[i] - ship[i];
+      if (p.backlog_cap(i) >= 0) b2 = min(b2, p.backlog_cap(i));
+      const int im = p.inv_max(i);
+      const int ou2 = min(max(ou[i] + order[i] - acq[i], 0), im);
+      const int inv2 = min(max(inv[i] + acq[i] - ship[i], 0), im);
+      prof[i] = ((p.sell(i) * (double)ship[i] - p.buy(i) * (double)order[i]) -
+                 p.stock_cost(i) * fabs((double)inv2 - p.inv_target(i))) -
+                p.backlog_cost(i) * (double)b2;
+      bl[i] = b2; ou[i] = ou2; inv[i] = inv2;
+      push[i] = (i == p.factory()) ? order[i] : sto[i];
+    }
+  }
+  // reward (IM_env.py:372 np.sum order; MAIM_env.py:418-434)
+  rew = 0.0;
+  if (p.reward_mode() != IMENV_REWARD_INDEPENDENT) {
+    if (p.reward_mode() == IMENV_REWARD_SHARED_MEAN || N < 8) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) if (i < N) rew += prof[i];
+      if (p.reward_mode() == IMENV_REWARD_SHARED_MEAN) rew = (p.inv_n() != 0.0) ? rew * p.inv_n() : rew / (double)N;
+    } else {
+      double r8[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r8[j] = (j < NT) ? prof[j < NT ? j : 0] : 0.0;
+      const int full = N - (N % 8);
+#pragma unroll
+      for (int i0 = 8; i0 < NT; i0 += 8) {
+        if (i0 < full) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) if (i0 + j < NT) r8[j] += prof[(i0 + j) < NT ? i0 + j : 0];
+        }
+      }
+      rew = ((r8[0] + r8[1]) + (r8[2] + r8[3])) + ((r8[4] + r8[5]) + (r8[6] + r8[7]));
+#pragma unroll
+      for (int i = 8; i < NT; ++i) if (i >= full && i < N) rew += prof[i];
+    }
+  }
+
+}
+
 // ---------------------------------------------------------------- step body
 // Structure: (A) issue every load that does not depend on this step's arithmetic (raw words),
 // (B) compute in registers, (C) store; float32 BASE observations are staged through LDS so the
@@ -430,7 +630,6 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   const int64_t n = A.n;
   const bool valid = e < n;
   const int N = p.N();
-  const int T = p.T();
   const int np = p.np();
   const int t = A.t;
   const bool poisson = p.demand_layout() == IMENV_LAYOUT_DRAW && p.demand_dist() == IMENV_DEMAND_POISSON;
@@ -568,184 +767,38 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
     if (i >= N || t < p.delay(i < N ? i : 0)) arr[i] = 0;   // nothing shipped d periods ago yet
   }
 
-  // ================= (B) compute
-  const double a = p.a();
-  const double bma = p.bma();
-  int order[NT], dem[NT], acq[NT], ship[NT], sto[NT], cout[NT], push[NT];
-  double prof[NT];
-  // order decode (IM_env.py:298-302; MAIM_env.py:340-347). Division by b - a is replaced by
-  // an exact multiply when b - a is a power of two (inv_bma != 0).
+  // per-period inputs that do not come from the state rows: customer demand (layout + noise) and
+  // the noisy-delay deferral decision
+  int cust[NT];
+  bool defer[NT];
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
-    order[i] = 0;
-    if (i < N) {
-      const double om = (double)p.order_max(i);
-      double v = x[i];
-      if (p.std_actions()) {
-        const double q = (x[i] - a) * (om - 0.0);
-        v = (p.inv_bma() != 0.0 ? q * p.inv_bma() : q / bma) + 0.0;
-      }
-      const double o = p.clip_round() ? rint(fmin(fmax(v, 0.0), om)) : fmin(fmax(rint(v), 0.0), om);
-      order[i] = (int)o;
-    }
-  }
-  // demand (IM_env.py:306-308, IM_div_env.py:380-387)
-#pragma unroll
-  for (int i = 0; i < NT; ++i) {
-    dem[i] = 0;
+    cust[i] = 0;
+    defer[i] = false;
     if (i < N) {
       const int r = p.retailer_slot(i);
       if (r >= 0) {
         int cd;
-        if (p.demand_layout() == IMENV_LAYOUT_PER_ENV) {
-          cd = cdem[i];
-        } else if (p.demand_layout() == IMENV_LAYOUT_BROADCAST) {
-          cd = A.demand[t * p.num_retailers() + r];
-        } else {
-          cd = cdraw[i];
-        }
+        if (p.demand_layout() == IMENV_LAYOUT_PER_ENV) cd = cdem[i];
+        else if (p.demand_layout() == IMENV_LAYOUT_BROADCAST) cd = A.demand[t * p.num_retailers() + r];
+        else cd = cdraw[i];
         if (p.noisy_demand()) {   // IM_div_env.py:246-255: double, then zero
           if (nd_double[i]) cd = 2 * cd;
           if (nd_zero[i]) cd = 0;
         }
-        dem[i] = min(cd, p.inv_max(i));
-      } else {
-        int s = 0;
-#pragma unroll
-        for (int c = 0; c < NT; ++c)
-          if (c < N && p.demand_parent(c) == i) s += order[c];
-        dem[i] = s;
+        cust[i] = cd;
       }
+      if (p.noisy_delay() && t >= p.delay(i)) defer[i] = p.has_delay_u() ? (du[i] <= A.noisy_delay_thr) : nd_delay[i];
     }
   }
-  // arrivals (IM_env.py:376-414); noisy delay defers the whole arrival (plus any carried amount)
-#pragma unroll
-  for (int i = 0; i < NT; ++i) {
-    acq[i] = ship[i] = cout[i] = 0;
-    if (i < N) {
-      int q = arr[i] + cin[i];
-      if (p.noisy_delay() && t >= p.delay(i)) {
-        bool extra;
-        if (p.has_delay_u()) extra = du[i] <= A.noisy_delay_thr;
-        else extra = nd_delay[i];
-        if (extra && t < T - 1) { cout[i] = q; q = 0; }
-      }
-      acq[i] = q;
-      ship[i] = min(bl[i] + dem[i], inv[i] + acq[i]);   // IM_env.py:315
-    }
-  }
-  // shipments into each node: a single-child parent's whole shipment, else the split
-#pragma unroll
-  for (int c = 0; c < NT; ++c) {
-    sto[c] = 0;
-    if (c < N) {
-      const int par = p.single_parent(c);
-      if (par >= 0) sto[c] = sel<NT>(ship, par);
-    }
-  }
-  bool split_ok = true;
-  if constexpr (MC > 0) {
-#pragma unroll
-    for (int si = 0; si < NT; ++si) {
-      if (si >= p.num_split()) break;
-      const int q = p.split_node(si);
-      const int m = p.num_children(q);
-      const int shp = sel<NT>(ship, q), dmp = sel<NT>(dem, q), blp = sel<NT>(bl, q);
-      int bto[MC], oc[MC], s[MC];
-#pragma unroll
-      for (int k = 0; k < MC; ++k) {
-        s[k] = 0; bto[k] = 0; oc[k] = 0;
-        if (k < m) {
-          const int c = p.child(q, k);
-          oc[k] = sel<NT>(order, c);
-          bto[k] = sel<NT>(btoc, c);
-        }
-      }
-      int amt = shp;
-      bool ok = true;
-      if (shp >= dmp) {
-        if (blp > 0) {        // backlog first, then outstanding orders (IM_div_env.py:409-454)
-          ok = rr_closed<MC, true>(m, bto, s, amt, p.split_limit(q, 0));
-          if (ok && amt > 0 && dmp > 0) {
-            int out[MC];
-#pragma unroll
-            for (int k = 0; k < MC; ++k) out[k] = oc[k];
-            ok = rr_closed<MC, true>(m, out, s, amt, p.split_limit(q, 1));
-#pragma unroll
-            for (int k = 0; k < MC; ++k) bto[k] += out[k];
-          }
-        } else {              // IM_div_env.py:457-460
-#pragma unroll
-          for (int k = 0; k < MC; ++k) s[k] += oc[k];
-        }
-      } else {
-        if (blp > 0) {        // IM_div_env.py:468-484
-          ok = rr_closed<MC, true>(m, bto, s, amt, p.split_limit(q, 2));
-        } else {              // IM_div_env.py:486-498: cap at order + backlog_to
-          int cap[MC];
-#pragma unroll
-          for (int k = 0; k < MC; ++k) cap[k] = oc[k] + bto[k];
-          ok = rr_closed<MC, false>(m, cap, s, amt, p.split_limit(q, 3));
-        }
-#pragma unroll
-        for (int k = 0; k < MC; ++k) bto[k] += oc[k] - s[k];   // IM_div_env.py:501-502
-      }
-      split_ok = split_ok && ok;
-#pragma unroll
-      for (int k = 0; k < MC; ++k) {
-        if (k < m) {
-          const int c = p.child(q, k);
-#pragma unroll
-          for (int j = 0; j < NT; ++j) {
-            sto[j] = (c == j) ? s[k] : sto[j];
-            btoc[j] = (c == j) ? bto[k] : btoc[j];
-          }
-        }
-      }
-    }
-  }
-  // balance equations and profit (IM_env.py:318-340, 362-367)
-#pragma unroll
-  for (int i = 0; i < NT; ++i) {
-    prof[i] = 0.0;
-    push[i] = 0;
-    if (i < N) {
-      int b2 = bl[i] + dem[i] - ship[i];
-      if (p.backlog_cap(i) >= 0) b2 = min(b2, p.backlog_cap(i));
-      const int im = p.inv_max(i);
-      const int ou2 = min(max(ou[i] + order[i] - acq[i], 0), im);
-      const int inv2 = min(max(inv[i] + acq[i] - ship[i], 0), im);
-      prof[i] = ((p.sell(i) * (double)ship[i] - p.buy(i) * (double)order[i]) -
-                 p.stock_cost(i) * fabs((double)inv2 - p.inv_target(i))) -
-                p.backlog_cost(i) * (double)b2;
-      bl[i] = b2; ou[i] = ou2; inv[i] = inv2;
-      push[i] = (i == p.factory()) ? order[i] : sto[i];
-    }
-  }
-  // reward (IM_env.py:372 np.sum order; MAIM_env.py:418-434)
-  double rew = 0.0;
-  if (p.reward_mode() != IMENV_REWARD_INDEPENDENT) {
-    if (p.reward_mode() == IMENV_REWARD_SHARED_MEAN || N < 8) {
-#pragma unroll
-      for (int i = 0; i < NT; ++i) if (i < N) rew += prof[i];
-      if (p.reward_mode() == IMENV_REWARD_SHARED_MEAN) rew = (p.inv_n() != 0.0) ? rew * p.inv_n() : rew / (double)N;
-    } else {
-      double r8[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) r8[j] = (j < NT) ? prof[j < NT ? j : 0] : 0.0;
-      const int full = N - (N % 8);
-#pragma unroll
-      for (int i0 = 8; i0 < NT; i0 += 8) {
-        if (i0 < full) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) if (i0 + j < NT) r8[j] += prof[(i0 + j) < NT ? i0 + j : 0];
-        }
-      }
-      rew = ((r8[0] + r8[1]) + (r8[2] + r8[3])) + ((r8[4] + r8[5]) + (r8[6] + r8[7]));
-#pragma unroll
-      for (int i = 8; i < NT; ++i) if (i >= full && i < N) rew += prof[i];
-    }
-  }
+
+  // ================= (B) compute
+  int order[NT], dem[NT], acq[NT], ship[NT], sto[NT], cout[NT], push[NT];
+  double prof[NT];
+  double rew;
+  bool split_ok;
+  step_core(p, t, x, cust, defer, arr, cin, inv, bl, ou, btoc, order, dem, acq, ship, sto, cout, push, prof, rew,
+            split_ok);
 
   // ================= (C) stores
   if (valid) {
@@ -891,6 +944,212 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
 #pragma unroll 1
       for (int f = 0; f < F; ++f) feature(f);
     }
+  }
+}
+
+// ---------------------------------------------------------------- fused base-stock rollout
+// One thread = one (policy, scenario) episode of T periods: base_restock_policy.py:24-45
+// (dfo_func) with the order-up-to policy of :4-21, evaluated through the same step_core as the
+// step kernel. State lives in registers for the whole episode; the lead-time queue (node i's d_i
+// in-transit slots) lives in LDS as [slot][thread] int32 (a wave's access is 64 consecutive
+// dwords: conflict-free). Metrics per episode:
+//   RETURN     sum_t reward, accumulated as the reference's eval loop does (inv_management.py:226-231)
+//   OBJECTIVE  dfo_func: -1/T * np.sum(pmf(customer_demand) * rewards), with np.sum's pairwise order
+//              over the flattened [R][T] products (base_restock_policy.py:41-45)
+//   INVENTORY / BACKLOG  sum_t sum_i of the post-step state; CUSTOMER_BACKLOG  sum_t of the
+//              retailers' backlog (inv_management.py:589-592)
+// Each block (one policy, BS scenarios) then reduces its metrics with wavefront shuffles + LDS
+// into one partial sum per block.
+template <int N8>
+__device__ __forceinline__ double pairwise8(const double (&r)[N8]) {
+  return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <class P, bool OBJ, bool LDS_TERMS>
+__device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, uint32_t* s_tab, int32_t* s_ring,
+                                             double* s_terms, double* s_red) {
+  constexpr int NT = P::NT;
+  constexpr int BS = P::BS;
+  const int tid = threadIdx.x;
+  const int N = p.N();
+  const int T = p.T();
+  const int R = p.num_retailers();
+  const int64_t pol = (int64_t)blockIdx.x / A.bpp;
+  const int64_t sb = (int64_t)blockIdx.x - pol * A.bpp;
+  const int64_t s = sb * BS + tid;
+  const bool valid = s < A.S;
+  const int64_t sl = valid ? s : A.S - 1;
+  const uint32_t gid = A.scen_offset + (uint32_t)sl;
+  const uint32_t ep = A.episode;
+  const uint64_t seed = p.seed();
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const bool draw = A.demand == nullptr;
+  const bool poisson = draw && p.demand_dist() == IMENV_DEMAND_POISSON;
+  p.stage_tables(s_tab, poisson);
+
+  double lvl[NT];
+  int inv[NT], bl[NT], ou[NT], btoc[NT], cin[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    lvl[i] = (i < N) ? A.policy[pol * N + i] : 0.0;
+    inv[i] = (i < N) ? p.init_inv(i) : 0;     // IM_env.py:221-224
+    bl[i] = ou[i] = btoc[i] = cin[i] = 0;
+  }
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+    if (i < N)
+      for (int k = 0; k < p.delay(i); ++k) s_ring[(p.ring_off(i) + k) * BS + tid] = 0;
+
+  const int n_terms = R * T;                       // np.sum over prob[R][T] * rewards[T]
+  const int full = n_terms >= 8 ? n_terms - (n_terms % 8) : 0;
+  double ret = 0.0;
+  double acc8[8], tail[7];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc8[j] = -0.0;      // -0.0 + x == x for every x: "+=" acts as the first assignment
+#pragma unroll
+  for (int j = 0; j < 7; ++j) tail[j] = 0.0;
+  int64_t inv_s = 0, bl_s = 0, cbl_s = 0;
+
+#pragma unroll 1
+  for (int t = 0; t < T; ++t) {
+    int cust[NT], arr[NT];
+    bool defer[NT];
+    double x[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      cust[i] = 0;
+      defer[i] = false;
+      arr[i] = 0;
+      x[i] = 0.0;
+      if (i < N) {
+        const int r = p.retailer_slot(i);
+        if (r >= 0) {
+          int cd;
+          if (!draw) {
+            cd = A.demand[((int64_t)t * R + r) * A.S + sl];
+          } else {
+            const uint32_t w = philox_word(gid, ep, (uint32_t)t, (STREAM_DEMAND << 16) | (uint32_t)(r >> 2), k0, k1,
+                                           r & 3);
+            if (poisson) {
+              cd = p.poisson_draw(w, s_tab);
+            } else {
+              const uint64_t rng = (uint64_t)(p.uniform_high() - p.uniform_low());
+              cd = p.uniform_low() + (int)(((uint64_t)w * rng) >> 32);
+            }
+            if (p.noisy_demand()) {     // IM_div_env.py:246-255: double, then zero
+              const uint32_t wd = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_DOUBLE << 16) | (uint32_t)(r >> 2), k0,
+                                              k1, r & 3);
+              const uint32_t wz = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_ZERO << 16) | (uint32_t)(r >> 2), k0,
+                                              k1, r & 3);
+              if ((uint64_t)wd < A.noisy_demand_thr32) cd = 2 * cd;
+              if ((uint64_t)wz < A.noisy_demand_thr32) cd = 0;
+            }
+          }
+          cust[i] = cd;
+        }
+        const int d = p.delay(i);
+        if (t >= d) arr[i] = s_ring[(p.ring_off(i) + t % d) * BS + tid];
+        if (p.noisy_delay() && t >= d)
+          defer[i] = (uint64_t)philox_word(gid, ep, (uint32_t)t, (STREAM_NOISY_DELAY << 16) | (uint32_t)(i >> 2), k0,
+                                           k1, i & 3) < A.noisy_delay_thr32;
+        // base_stock_policy (base_restock_policy.py:12-20): inv + order_u - backlog at this period,
+        // min(order_max, max(policy - inv_ech, 0)); the env then decodes it like any action
+        const double ie = (double)inv[i] + (double)ou[i] - (double)bl[i];
+        x[i] = fmin((double)p.order_max(i), fmax(lvl[i] - ie, 0.0));
+      }
+    }
+    int order[NT], dem[NT], acq[NT], ship[NT], sto[NT], cout[NT], push[NT];
+    double prof[NT];
+    double rew;
+    bool split_ok;
+    step_core(p, t, x, cust, defer, arr, cin, inv, bl, ou, btoc, order, dem, acq, ship, sto, cout, push, prof, rew,
+              split_ok);
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      if (i < N) {
+        const int d = p.delay(i);
+        s_ring[(p.ring_off(i) + t % d) * BS + tid] = push[i];
+        cin[i] = cout[i];
+        inv_s += inv[i];
+        bl_s += bl[i];
+        if (p.retailer_slot(i) >= 0) cbl_s += bl[i];
+      }
+    }
+    ret += rew;
+    if constexpr (OBJ) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const int r = (i < N) ? p.retailer_slot(i) : -1;
+        if (r >= 0) {
+          const int k = cust[i];
+          const double w = (k >= 0 && k < A.pmf_len) ? A.pmf[k] : 0.0;
+          const double term = w * rew;
+          const int idx = r * T + t;
+          if constexpr (LDS_TERMS) {
+            s_terms[idx * BS + tid] = term;
+          } else {                    // R == 1: terms arrive in index order
+            if (idx < full) {
+              const int j = idx & 7;
+#pragma unroll
+              for (int q = 0; q < 8; ++q) acc8[q] = (q == j) ? acc8[q] + term : acc8[q];
+            } else {
+              const int j = idx - full;
+#pragma unroll
+              for (int q = 0; q < 7; ++q) tail[q] = (q == j) ? term : tail[q];
+            }
+          }
+        }
+      }
+    }
+  }
+
+  double obj = 0.0;
+  if constexpr (OBJ) {
+    if constexpr (LDS_TERMS) {
+      for (int idx = 0; idx < full; ++idx) {
+        const double term = s_terms[idx * BS + tid];
+        const int j = idx & 7;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc8[q] = (q == j) ? acc8[q] + term : acc8[q];
+      }
+      for (int idx = full; idx < n_terms; ++idx) {
+        const double term = s_terms[idx * BS + tid];
+        const int j = idx - full;
+#pragma unroll
+        for (int q = 0; q < 7; ++q) tail[q] = (q == j) ? term : tail[q];
+      }
+    }
+    double sum = (n_terms >= 8) ? pairwise8(acc8) : 0.0;
+#pragma unroll
+    for (int q = 0; q < 7; ++q)
+      if (q < n_terms - full) sum += tail[q];
+    obj = (-1.0 / (double)T) * sum;               // -1 / env.num_periods * np.sum(...)
+  }
+
+  const double v[IMENV_NUM_STATS] = {ret, obj, (double)inv_s, (double)bl_s, (double)cbl_s};
+  const int64_t PS = A.P * A.S;
+  if (valid) {
+#pragma unroll
+    for (int m = 0; m < IMENV_NUM_STATS; ++m) A.ep[m * PS + pol * A.S + s] = v[m];
+  }
+  // block reduction: wavefront shuffles, then the waves' sums in order through LDS (deterministic)
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int m = 0; m < IMENV_NUM_STATS; ++m) {
+    const double w = wave_sum(valid ? v[m] : 0.0);
+    if (lane == 0) s_red[m * (BS / 64) + wv] = w;
+  }
+  __syncthreads();
+  if (tid < IMENV_NUM_STATS) {
+    double acc = 0.0;
+    for (int k = 0; k < BS / 64; ++k) acc += s_red[tid * (BS / 64) + k];
+    A.partial[((int64_t)tid * A.P + pol) * A.bpp + sb] = acc;
   }
 }
 

@@ -55,4 +55,24 @@ bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const st
 
 hipError_t jit_launch(const JitKernel& k, hipStream_t st, const SpecDev* sp, const StepArgs& A);
 
+// Fused base-stock rollout kernel (rollout_body): compile-time properties of one launch.
+struct RolloutFlags {
+  bool table = false;         // host demand table (else in-kernel draws)
+  bool noisy_delay = false;
+  bool noisy_demand = false;  // drawn demand only
+  bool objective = false;     // dfo_func objective (pmf given)
+  bool lds_terms = false;     // objective with > 1 retailer: [R][T] products kept in LDS
+  uint32_t key() const {
+    return (table ? 1u : 0u) | (noisy_delay ? 2u : 0u) | (noisy_demand ? 4u : 0u) | (objective ? 8u : 0u) |
+           (lds_terms ? 16u : 0u);
+  }
+};
+
+// Threads per block of the rollout kernel for this spec (0: does not fit LDS).
+int rollout_block_size(const SpecDev& d, const RolloutFlags& f);
+std::string jit_rollout_source(const SpecDev& d, int maxc, const RolloutFlags& f, int bs);
+bool jit_rollout_load(const SpecDev& d, int maxc, const RolloutFlags& f, const std::string& arch, JitKernel& out,
+                      std::string& msg);
+hipError_t jit_rollout_launch(const JitKernel& k, hipStream_t st, const SpecDev* sp, const RolloutArgs& A);
+
 }  // namespace imenv

@@ -133,7 +133,9 @@ void emit_obs_hooks(std::ostream& o, const SpecDev& d) {
 
 }  // namespace
 
-std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f) {
+namespace {
+// The JitSpec policy class: every accessor step_body / rollout_body use, as a constexpr.
+void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const JitFlags& f, int bs) {
   const ImEnvSpec& s = d.s;
   const int N = s.num_nodes;
   const int F = s.num_features;
@@ -141,7 +143,6 @@ std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f)
   for (int k = 0; k < F; ++k)
     if (s.feat_group[k] == IMENV_G_DEMAND_HIST || s.feat_group[k] == IMENV_G_ORDER_HIST) uses_hist = true;
   const bool inline_tab = d.table_len <= kInlineTable;
-  std::ostringstream o;
   o << "#include \"imenv_device.h\"\n"
        "// generated by imenv_jit.hip: every spec value is a compile-time constant\n"
        "struct JitSpec {\n";
@@ -151,10 +152,11 @@ std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f)
     << "  static constexpr bool EXACT = true;\n"
     << "  static constexpr bool JIT = true;\n"
     << "  static constexpr int TAB_LDS = " << (inline_tab ? 1 : IMENV_TABLE_MAX) << ";\n"
-    << "  static constexpr int BS = " << jit_block_size() << ";\n"
+    << "  static constexpr int BS = " << bs << ";\n"
+    << "  static constexpr int RING = " << d.ring_total << ";\n"
     << "  using ST = " << (d.es == 1 ? "uint8_t" : d.es == 2 ? "int16_t" : "int32_t") << ";\n"
     << "  const imenv::SpecDev* __restrict__ sp;\n"
-    << "  __device__ JitSpec(const imenv::SpecDev* __restrict__ s, const imenv::StepArgs&) : sp(s) {}\n";
+    << "  template <class X> __device__ JitSpec(const imenv::SpecDev* __restrict__ s, const X&) : sp(s) {}\n";
   auto sc = [&](const char* type, const char* name, const std::string& v) {
     o << "  __device__ static constexpr " << type << " " << name << "() { return " << v << "; }\n";
   };
@@ -231,10 +233,16 @@ std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f)
          "    return lo;\n  }\n"
          "  __device__ void stage_tables(uint32_t* s_tab, bool poisson) const {\n"
          "    if (poisson) { for (int k = threadIdx.x; k < "
-      << d.table_len << "; k += 256) s_tab[k] = sp->table[k]; __syncthreads(); }\n  }\n";
+      << d.table_len << "; k += BS) s_tab[k] = sp->table[k]; __syncthreads(); }\n  }\n";
   }
-  o << "};\n\n"
-       "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
+  o << "};\n\n";
+}
+}  // namespace
+
+std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f) {
+  std::ostringstream o;
+  emit_policy(o, d, maxc, base, f, jit_block_size());
+  o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
        "imenv_step_jit(const imenv::SpecDev* __restrict__ sp, const imenv::StepArgs A) {\n"
        "  __shared__ uint32_t s_tab[JitSpec::TAB_LDS];\n"
        "  __shared__ __attribute__((aligned(16))) float s_obs[imenv::stage_floats<JitSpec>()];\n"
@@ -311,9 +319,9 @@ std::shared_ptr<const std::vector<char>> jit_compile(const std::string& src, con
   return ins.first->second;
 }
 
-bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const std::string& arch, JitKernel& out,
-              std::string& msg) {
-  const std::string src = jit_source(d, maxc, base, f);
+namespace {
+bool load_module(const std::string& src, const std::string& arch, const char* fn_name, JitKernel& out,
+                 std::string& msg) {
   auto code = jit_compile(src, arch, msg);
   if (!code) return false;
   hipModule_t mod = nullptr;
@@ -323,7 +331,7 @@ bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const st
     return false;
   }
   hipFunction_t fn = nullptr;
-  e = hipModuleGetFunction(&fn, mod, "imenv_step_jit");
+  e = hipModuleGetFunction(&fn, mod, fn_name);
   if (e != hipSuccess) {
     (void)hipModuleUnload(mod);
     msg = std::string("hipModuleGetFunction: ") + hipGetErrorString(e);
@@ -331,6 +339,14 @@ bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const st
   }
   out.mod = mod;
   out.fn = fn;
+  return true;
+}
+}  // namespace
+
+bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const std::string& arch, JitKernel& out,
+              std::string& msg) {
+  const std::string src = jit_source(d, maxc, base, f);
+  if (!load_module(src, arch, "imenv_step_jit", out, msg)) return false;
   out.bs = jit_block_size();
   char tag[160];
   std::snprintf(tag, sizeof tag, "jit:imenv_step_jit[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,%zuB]",
@@ -344,6 +360,65 @@ hipError_t jit_launch(const JitKernel& k, hipStream_t st, const SpecDev* sp, con
   StepArgs av = A;
   void* args[] = {&spv, &av};
   const unsigned grid = (unsigned)((A.n + k.bs - 1) / k.bs);
+  return hipModuleLaunchKernel(k.fn, grid, 1, 1, (unsigned)k.bs, 1, 1, 0, st, args, nullptr);
+}
+
+// ---------------------------------------------------------------- fused base-stock rollout
+int rollout_block_size(const SpecDev& d, const RolloutFlags& f) {
+  // LDS per thread: the in-transit queue (int32 per slot) and, for the multi-retailer objective,
+  // the [R][T] products np.sum needs in index order. Largest block whose LDS fits 64 KiB.
+  const int per = 4 * d.ring_total + (f.lds_terms ? 8 * d.s.num_retailers * d.s.num_periods : 0);
+  for (int bs : {256, 128, 64})
+    if (bs * per + 4 * IMENV_TABLE_MAX + 8 * IMENV_NUM_STATS * 4 <= 65536) return bs;
+  return 0;
+}
+
+std::string jit_rollout_source(const SpecDev& d, int maxc, const RolloutFlags& f, int bs) {
+  JitFlags jf;
+  jf.noisy_delay = f.noisy_delay;
+  jf.noisy_demand = f.noisy_demand;
+  jf.demand_layout = f.table ? IMENV_LAYOUT_PER_ENV : IMENV_LAYOUT_DRAW;
+  std::ostringstream o;
+  emit_policy(o, d, maxc, false, jf, bs);
+  const int terms = f.lds_terms ? d.s.num_retailers * d.s.num_periods : 1;
+  o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
+       "imenv_rollout_jit(const imenv::SpecDev* __restrict__ sp, const imenv::RolloutArgs A) {\n"
+       "  __shared__ uint32_t s_tab[JitSpec::TAB_LDS];\n"
+       "  __shared__ int32_t s_ring[JitSpec::RING * JitSpec::BS];\n"
+       "  __shared__ double s_terms["
+    << terms
+    << " * JitSpec::BS];\n"
+       "  __shared__ double s_red[IMENV_NUM_STATS * (JitSpec::BS / 64)];\n"
+       "  const JitSpec p(sp, A);\n"
+       "  imenv::rollout_body<JitSpec, "
+    << blit(f.objective) << ", " << blit(f.lds_terms)
+    << ">(p, A, s_tab, s_ring, s_terms, s_red);\n"
+       "}\n";
+  return o.str();
+}
+
+bool jit_rollout_load(const SpecDev& d, int maxc, const RolloutFlags& f, const std::string& arch, JitKernel& out,
+                      std::string& msg) {
+  const int bs = rollout_block_size(d, f);
+  if (bs == 0) {
+    msg = "rollout: in-transit queue + objective terms exceed 64 KiB of LDS at 64 threads per block";
+    return false;
+  }
+  const std::string src = jit_rollout_source(d, maxc, f, bs);
+  if (!load_module(src, arch, "imenv_rollout_jit", out, msg)) return false;
+  out.bs = bs;
+  char tag[160];
+  std::snprintf(tag, sizeof tag, "jit:imenv_rollout_jit[N=%d,MC=%d,es=%d,flags=0x%x,bs=%d,%zuB]", d.s.num_nodes,
+                maxc, d.es, f.key(), bs, src.size());
+  out.tag = tag;
+  return true;
+}
+
+hipError_t jit_rollout_launch(const JitKernel& k, hipStream_t st, const SpecDev* sp, const RolloutArgs& A) {
+  const SpecDev* spv = sp;
+  RolloutArgs av = A;
+  void* args[] = {&spv, &av};
+  const unsigned grid = (unsigned)(A.P * A.bpp);
   return hipModuleLaunchKernel(k.fn, grid, 1, 1, (unsigned)k.bs, 1, 1, 0, st, args, nullptr);
 }
 

@@ -28,6 +28,9 @@ OBS_ZERO, OBS_RAW, OBS_SCALED, OBS_CLAMP_SCALED = 0, 1, 2, 3
 DEMAND_CUSTOM, DEMAND_POISSON, DEMAND_UNIFORM = 1, 2, 3
 LAYOUT_DRAW, LAYOUT_PER_ENV, LAYOUT_BROADCAST = 0, 1, 2
 F32, F64 = 0, 1
+STAT_RETURN, STAT_OBJECTIVE, STAT_INVENTORY, STAT_BACKLOG, STAT_CUSTOMER_BACKLOG = range(5)
+NUM_STATS = 5
+STAT_NAMES = ("return", "objective", "inventory", "backlog", "customer_backlog")
 
 
 class ImEnvNativeError(RuntimeError):
@@ -60,6 +63,13 @@ class ImEnvInfo(ctypes.Structure):
                 ("profit", c_void_p), ("ship_to", c_void_p), ("backlog_to", c_void_p)]
 
 
+class ImEnvRollout(ctypes.Structure):
+    _fields_ = [("policy", c_void_p), ("num_policies", c_int64), ("num_scenarios", c_int64),
+                ("demand", c_void_p), ("scenario_offset", c_int64), ("episode", c_int64),
+                ("demand_pmf", c_void_p), ("pmf_len", c_int32), ("noisy_delay", c_int32),
+                ("noisy_delay_threshold", c_double), ("episode_stats", c_void_p), ("policy_stats", c_void_p)]
+
+
 # (name, restype, argtypes) for every symbol include/imenv.h declares
 SYMBOLS = [
     ("imenv_create", c_int, [POINTER(ImEnvSpec), c_int64, c_int64, c_int, POINTER(c_void_p)]),
@@ -67,6 +77,7 @@ SYMBOLS = [
                             c_void_p]),
     ("imenv_step", c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, POINTER(ImEnvInfo),
                            POINTER(c_int32), c_void_p]),
+    ("imenv_base_stock_rollout", c_int, [c_void_p, POINTER(ImEnvRollout), c_void_p]),
     ("imenv_get_state", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_int32), c_void_p]),
     ("imenv_get_errors", c_int, [c_void_p, c_void_p, POINTER(c_uint32), c_void_p]),
     ("imenv_dims", c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),

@@ -20,8 +20,12 @@ def decode_config(cfg):
     return out
 
 
+NON_CASE = ("base_stock",)      # tools/gen_base_stock_fixtures.py, loaded by load_base_stock()
+
+
 def case_names():
-    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+    names = (os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+    return sorted(n for n in names if n not in NON_CASE)
 
 
 def load_case(name):
@@ -46,3 +50,18 @@ def load_adaptor_case(name):
     d = {k: z[k] for k in z.files}
     meta = json.loads(str(d.pop("meta")))
     return meta, d
+
+
+def load_base_stock():
+    """tests/golden/base_stock.npz (tools/gen_base_stock_fixtures.py): {case: {field: array}}, meta."""
+    z = np.load(os.path.join(GOLDEN, "base_stock.npz"), allow_pickle=False)
+    meta = json.loads(str(z["meta"]))
+    cases = {}
+    for k in z.files:
+        if k == "meta":
+            continue
+        c, f = k.split("/")
+        cases.setdefault(c, {})[f] = z[k]
+    for c in meta:
+        meta[c]["config"] = decode_config(meta[c]["config"])
+    return meta, cases
