@@ -211,7 +211,7 @@ typedef struct ImEnvRollout {
   int32_t pmf_len;
   int32_t noisy_delay;        /* reset(noisy_delay=True, noisy_delay_threshold) (IM_env.py:180-182) */
   double noisy_delay_threshold;
-  double* episode_stats;      /* out [IMENV_NUM_STATS][P][S], or NULL */
+  double* episode_stats;      /* out [IMENV_NUM_STATS][P][S], or NULL (then only policy_stats) */
   double* policy_stats;       /* out [P][IMENV_NUM_STATS][2]: np.mean, np.std over the S episodes, or NULL */
 } ImEnvRollout;
 
@@ -300,7 +300,7 @@ int imenv_kernel_info(const ImEnv* env, char* buf, int64_t len);
  * `spec` for `arch` (e.g. "gfx950"); flags = bit0 f64 actions, bit1 f64 obs, bit2 noisy delay,
  * bit3 noisy demand, bit4 host-fed delay uniforms, bits 5-11 demand layout. With bit 12 set it
  * compiles the base-stock rollout kernel instead: bit13 demand table, bit14 noisy delay, bit15 noisy
- * demand, bit16 objective, bit17 objective terms in LDS (> 1 retailer). `log` receives "ok" or
+ * demand, bit16 objective. `log` receives "ok" or
  * the compiler log. */
 int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, char* log, int64_t log_len);
 

@@ -65,16 +65,15 @@ __global__ void __launch_bounds__(256) imenv_unpack_kernel(const ST* __restrict_
   for (int i = 0; i < N; ++i) dst[i * n + e] = (int32_t)src[e * np + i];
 }
 
-// policy_stats of a base-stock rollout: one block per policy and metric. np.mean over the S
-// episodes from the rollout kernel's per-block partial sums, then np.std's second pass over the
-// per-episode values: mean(|x - mean|^2). Strided per-thread sums, wavefront shuffles and a fixed
+// policy_stats of a base-stock rollout: one block per (policy, metric) merges the rollout kernel's
+// per-block (sum, M2 about the block mean, count) triples with Chan et al.'s pairwise update
+//   M2 = sum_b M2_b + sum_b n_b (mean_b - mean)^2,  mean = sum_b sum_b / S
+// -> np.mean and np.std (population). Strided per-thread sums, wavefront shuffles and a fixed
 // wave order through LDS: deterministic, the same bits for the same inputs.
-__global__ void __launch_bounds__(256) imenv_rollout_stats_kernel(const double* __restrict__ ep,
-                                                                  const double* __restrict__ partial,
+__global__ void __launch_bounds__(256) imenv_rollout_stats_kernel(const double* __restrict__ partial,
                                                                   double* __restrict__ out, int64_t P, int64_t S,
                                                                   int64_t bpp) {
   __shared__ double s_w[4];
-  __shared__ double s_mean;
   const int64_t pol = blockIdx.x;
   const int m = blockIdx.y;
   const int tid = threadIdx.x;
@@ -86,19 +85,19 @@ __global__ void __launch_bounds__(256) imenv_rollout_stats_kernel(const double* 
     __syncthreads();
     return r;
   };
+  const double* pb = partial + ((int64_t)m * P + pol) * bpp * 3;
   double a = 0.0;
-  for (int64_t k = tid; k < bpp; k += 256) a += partial[((int64_t)m * P + pol) * bpp + k];
+  for (int64_t k = tid; k < bpp; k += 256) a += pb[3 * k];
   const double mean = block_sum(a) / (double)S;
-  if (tid == 0) s_mean = mean;
-  const double* x = ep + ((int64_t)m * P + pol) * S;
   double q = 0.0;
-  for (int64_t k = tid; k < S; k += 256) {
-    const double d = x[k] - mean;
-    q += d * d;
+  for (int64_t k = tid; k < bpp; k += 256) {
+    const double nb = pb[3 * k + 2];
+    const double d = pb[3 * k] / nb - mean;
+    q += pb[3 * k + 1] + nb * (d * d);
   }
   const double var = block_sum(q) / (double)S;
   if (tid == 0) {
-    out[(pol * IMENV_NUM_STATS + m) * 2 + 0] = s_mean;
+    out[(pol * IMENV_NUM_STATS + m) * 2 + 0] = mean;
     out[(pol * IMENV_NUM_STATS + m) * 2 + 1] = sqrt(var);
   }
 }
@@ -373,8 +372,6 @@ struct ImEnv {
   std::string last_kernel;
   // base-stock rollout: kernels per RolloutFlags, scratch for per-episode metrics and block sums
   std::unordered_map<uint32_t, imenv::JitKernel> roll_k;
-  double* d_roll_ep = nullptr;
-  size_t roll_ep_cap = 0;
   double* d_roll_part = nullptr;
   size_t roll_part_cap = 0;
   std::string last_rollout;
@@ -393,7 +390,7 @@ void imenv_destroy(ImEnv* h) {
   (void)hipSetDevice(h->device);
   void* ptrs[] = {h->d_spec, h->d_inv, h->d_bl, h->d_ou, h->d_ring, h->d_carry, h->d_bto, h->d_hist_d,
                   h->d_hist_o, h->d_demand, h->d_delay_u, h->d_err, h->d_err_any, h->d_lut32, h->d_lut64,
-                  h->d_episode, h->d_roll_ep, h->d_roll_part};
+                  h->d_episode, h->d_roll_part};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& kv : h->jit_k)
@@ -640,7 +637,6 @@ int imenv_base_stock_rollout(ImEnv* h, const ImEnvRollout* r, void* stream) {
   f.noisy_delay = r->noisy_delay != 0;
   f.noisy_demand = !f.table && s.noisy_demand != 0;
   f.objective = r->demand_pmf != nullptr;
-  f.lds_terms = f.objective && s.num_retailers > 1;
   auto it = h->roll_k.find(f.key());
   if (it == h->roll_k.end()) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -658,17 +654,7 @@ int imenv_base_stock_rollout(ImEnv* h, const ImEnvRollout* r, void* stream) {
   const int64_t bpp = (S + k.bs - 1) / k.bs;
   if (P * bpp > 0x7FFFFFFFll) return fail(IMENV_E_INVALID, "num_policies * ceil(num_scenarios / block) too large");
   double* ep = r->episode_stats;
-  if (!ep) {
-    const size_t need = (size_t)IMENV_NUM_STATS * P * S;
-    if (h->roll_ep_cap < need) {
-      if (h->d_roll_ep) { HIPCHK(hipStreamSynchronize(st)); HIPCHK(hipFree(h->d_roll_ep)); h->d_roll_ep = nullptr; }
-      int rc = alloc(&h->d_roll_ep, need);
-      if (rc) return rc;
-      h->roll_ep_cap = need;
-    }
-    ep = h->d_roll_ep;
-  }
-  const size_t pneed = (size_t)IMENV_NUM_STATS * P * bpp;
+  const size_t pneed = (size_t)IMENV_NUM_STATS * P * bpp * 3;
   if (h->roll_part_cap < pneed) {
     if (h->d_roll_part) { HIPCHK(hipStreamSynchronize(st)); HIPCHK(hipFree(h->d_roll_part)); h->d_roll_part = nullptr; }
     int rc = alloc(&h->d_roll_part, pneed);
@@ -695,7 +681,7 @@ int imenv_base_stock_rollout(ImEnv* h, const ImEnvRollout* r, void* stream) {
   HIPCHK(imenv::jit_rollout_launch(k, st, h->d_spec, A));
   h->last_rollout = k.tag;
   if (r->policy_stats) {
-    hipLaunchKernelGGL(imenv_rollout_stats_kernel, dim3((unsigned)P, IMENV_NUM_STATS), dim3(256), 0, st, ep,
+    hipLaunchKernelGGL(imenv_rollout_stats_kernel, dim3((unsigned)P, IMENV_NUM_STATS), dim3(256), 0, st,
                        h->d_roll_part, r->policy_stats, P, S, bpp);
     HIPCHK(hipGetLastError());
   }
@@ -853,7 +839,6 @@ int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, cha
     rf.noisy_delay = rk & 2u;
     rf.noisy_demand = rk & 4u;
     rf.objective = rk & 8u;
-    rf.lds_terms = rk & 16u;
     const int bs = imenv::rollout_block_size(d, rf);
     if (bs == 0) return fail(IMENV_E_UNSUPPORTED, "rollout does not fit LDS");
     src = imenv::jit_rollout_source(d, maxc, rf, bs);

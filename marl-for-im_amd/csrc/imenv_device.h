@@ -122,8 +122,8 @@ struct RolloutArgs {
   const double* policy;       // [P][N] order-up-to levels
   const int32_t* demand;      // [T][R][S] customer demand per scenario, or null: drawn in-kernel
   const double* pmf;          // [pmf_len] dfo_func weight of a customer-demand value (objective only)
-  double* ep;                 // [IMENV_NUM_STATS][P][S] per-episode metrics
-  double* partial;            // [IMENV_NUM_STATS][P][bpp] per-block sums (wavefront reductions)
+  double* ep;                 // [IMENV_NUM_STATS][P][S] per-episode metrics, or null
+  double* partial;            // [IMENV_NUM_STATS][P][bpp][3] per-block (sum, M2, count)
   int64_t S;                  // scenarios per policy
   int64_t P;                  // policies
   int64_t bpp;                // blocks per policy = ceil(S / BS)
@@ -952,28 +952,42 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
 // (dfo_func) with the order-up-to policy of :4-21, evaluated through the same step_core as the
 // step kernel. State lives in registers for the whole episode; the lead-time queue (node i's d_i
 // in-transit slots) lives in LDS as [slot][thread] int32 (a wave's access is 64 consecutive
-// dwords: conflict-free). Metrics per episode:
+// dwords: conflict-free), as do the Poisson table and the pmf weights. Metrics per episode:
 //   RETURN     sum_t reward, accumulated as the reference's eval loop does (inv_management.py:226-231)
-//   OBJECTIVE  dfo_func: -1/T * np.sum(pmf(customer_demand) * rewards), with np.sum's pairwise order
-//              over the flattened [R][T] products (base_restock_policy.py:41-45)
+//   OBJECTIVE  dfo_func: -1/T * np.sum(pmf(customer_demand) * rewards), in np.sum's pairwise order
+//              over the flattened [R][T] products (base_restock_policy.py:41-45). The products of
+//              retailer row r come after all of row r-1 in that order, so with R > 1 retailers the
+//              episode is replayed R times (pass r adds row r; the replay is deterministic): no
+//              per-thread buffer of R*T terms, full occupancy.
 //   INVENTORY / BACKLOG  sum_t sum_i of the post-step state; CUSTOMER_BACKLOG  sum_t of the
 //              retailers' backlog (inv_management.py:589-592)
-// Each block (one policy, BS scenarios) then reduces its metrics with wavefront shuffles + LDS
-// into one partial sum per block.
-template <int N8>
-__device__ __forceinline__ double pairwise8(const double (&r)[N8]) {
-  return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-}
-
+// Each block (one policy, BS scenarios) then reduces every metric with wavefront shuffles + LDS to
+// (sum, M2 about the block mean, count): the stats kernel merges blocks with Chan's pairwise update
+// (stable, deterministic).
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 
-template <class P, bool OBJ, bool LDS_TERMS>
+// Sum over the block's threads: wave shuffles, then the waves' sums in a fixed order (deterministic).
+// Every thread gets the result. s_red holds BS / 64 doubles.
+template <int BS>
+__device__ __forceinline__ double block_sum(double v, double* s_red) {
+  const int tid = threadIdx.x;
+  const double w = wave_sum(v);
+  if ((tid & 63) == 0) s_red[tid >> 6] = w;
+  __syncthreads();
+  double r = 0.0;
+#pragma unroll
+  for (int k = 0; k < BS / 64; ++k) r += s_red[k];
+  __syncthreads();
+  return r;
+}
+
+template <class P, bool OBJ>
 __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, uint32_t* s_tab, int32_t* s_ring,
-                                             double* s_terms, double* s_red) {
+                                             double* s_pmf, int pmf_lds, double* s_red) {
   constexpr int NT = P::NT;
   constexpr int BS = P::BS;
   const int tid = threadIdx.x;
@@ -992,19 +1006,15 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, u
   const bool draw = A.demand == nullptr;
   const bool poisson = draw && p.demand_dist() == IMENV_DEMAND_POISSON;
   p.stage_tables(s_tab, poisson);
+  const int pmf_n = A.pmf_len < pmf_lds ? A.pmf_len : pmf_lds;
+  if constexpr (OBJ) {
+    for (int k = tid; k < pmf_n; k += BS) s_pmf[k] = A.pmf[k];
+    __syncthreads();
+  }
 
   double lvl[NT];
-  int inv[NT], bl[NT], ou[NT], btoc[NT], cin[NT];
 #pragma unroll
-  for (int i = 0; i < NT; ++i) {
-    lvl[i] = (i < N) ? A.policy[pol * N + i] : 0.0;
-    inv[i] = (i < N) ? p.init_inv(i) : 0;     // IM_env.py:221-224
-    bl[i] = ou[i] = btoc[i] = cin[i] = 0;
-  }
-#pragma unroll
-  for (int i = 0; i < NT; ++i)
-    if (i < N)
-      for (int k = 0; k < p.delay(i); ++k) s_ring[(p.ring_off(i) + k) * BS + tid] = 0;
+  for (int i = 0; i < NT; ++i) lvl[i] = (i < N) ? A.policy[pol * N + i] : 0.0;
 
   const int n_terms = R * T;                       // np.sum over prob[R][T] * rewards[T]
   const int full = n_terms >= 8 ? n_terms - (n_terms % 8) : 0;
@@ -1016,84 +1026,102 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, u
   for (int j = 0; j < 7; ++j) tail[j] = 0.0;
   int64_t inv_s = 0, bl_s = 0, cbl_s = 0;
 
+  const int passes = OBJ ? R : 1;
 #pragma unroll 1
-  for (int t = 0; t < T; ++t) {
-    int cust[NT], arr[NT];
-    bool defer[NT];
-    double x[NT];
+  for (int pass = 0; pass < passes; ++pass) {
+    int inv[NT], bl[NT], ou[NT], btoc[NT], cin[NT];
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
-      cust[i] = 0;
-      defer[i] = false;
-      arr[i] = 0;
-      x[i] = 0.0;
-      if (i < N) {
-        const int r = p.retailer_slot(i);
-        if (r >= 0) {
-          int cd;
-          if (!draw) {
-            cd = A.demand[((int64_t)t * R + r) * A.S + sl];
-          } else {
-            const uint32_t w = philox_word(gid, ep, (uint32_t)t, (STREAM_DEMAND << 16) | (uint32_t)(r >> 2), k0, k1,
-                                           r & 3);
-            if (poisson) {
-              cd = p.poisson_draw(w, s_tab);
-            } else {
-              const uint64_t rng = (uint64_t)(p.uniform_high() - p.uniform_low());
-              cd = p.uniform_low() + (int)(((uint64_t)w * rng) >> 32);
-            }
-            if (p.noisy_demand()) {     // IM_div_env.py:246-255: double, then zero
-              const uint32_t wd = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_DOUBLE << 16) | (uint32_t)(r >> 2), k0,
-                                              k1, r & 3);
-              const uint32_t wz = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_ZERO << 16) | (uint32_t)(r >> 2), k0,
-                                              k1, r & 3);
-              if ((uint64_t)wd < A.noisy_demand_thr32) cd = 2 * cd;
-              if ((uint64_t)wz < A.noisy_demand_thr32) cd = 0;
-            }
-          }
-          cust[i] = cd;
-        }
-        const int d = p.delay(i);
-        if (t >= d) arr[i] = s_ring[(p.ring_off(i) + t % d) * BS + tid];
-        if (p.noisy_delay() && t >= d)
-          defer[i] = (uint64_t)philox_word(gid, ep, (uint32_t)t, (STREAM_NOISY_DELAY << 16) | (uint32_t)(i >> 2), k0,
-                                           k1, i & 3) < A.noisy_delay_thr32;
-        // base_stock_policy (base_restock_policy.py:12-20): inv + order_u - backlog at this period,
-        // min(order_max, max(policy - inv_ech, 0)); the env then decodes it like any action
-        const double ie = (double)inv[i] + (double)ou[i] - (double)bl[i];
-        x[i] = fmin((double)p.order_max(i), fmax(lvl[i] - ie, 0.0));
-      }
+      inv[i] = (i < N) ? p.init_inv(i) : 0;     // IM_env.py:221-224
+      bl[i] = ou[i] = btoc[i] = cin[i] = 0;
     }
-    int order[NT], dem[NT], acq[NT], ship[NT], sto[NT], cout[NT], push[NT];
-    double prof[NT];
-    double rew;
-    bool split_ok;
-    step_core(p, t, x, cust, defer, arr, cin, inv, bl, ou, btoc, order, dem, acq, ship, sto, cout, push, prof, rew,
-              split_ok);
 #pragma unroll
-    for (int i = 0; i < NT; ++i) {
-      if (i < N) {
-        const int d = p.delay(i);
-        s_ring[(p.ring_off(i) + t % d) * BS + tid] = push[i];
-        cin[i] = cout[i];
-        inv_s += inv[i];
-        bl_s += bl[i];
-        if (p.retailer_slot(i) >= 0) cbl_s += bl[i];
-      }
-    }
-    ret += rew;
-    if constexpr (OBJ) {
+    for (int i = 0; i < NT; ++i)
+      if (i < N)
+        for (int k = 0; k < p.delay(i); ++k) s_ring[(p.ring_off(i) + k) * BS + tid] = 0;
+
+#pragma unroll 1
+    for (int t = 0; t < T; ++t) {
+      int cust[NT], arr[NT];
+      bool defer[NT];
+      double x[NT];
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
-        const int r = (i < N) ? p.retailer_slot(i) : -1;
-        if (r >= 0) {
-          const int k = cust[i];
-          const double w = (k >= 0 && k < A.pmf_len) ? A.pmf[k] : 0.0;
-          const double term = w * rew;
-          const int idx = r * T + t;
-          if constexpr (LDS_TERMS) {
-            s_terms[idx * BS + tid] = term;
-          } else {                    // R == 1: terms arrive in index order
+        cust[i] = 0;
+        defer[i] = false;
+        arr[i] = 0;
+        x[i] = 0.0;
+        if (i < N) {
+          const int r = p.retailer_slot(i);
+          if (r >= 0) {
+            int cd;
+            if (!draw) {
+              cd = A.demand[((int64_t)t * R + r) * A.S + sl];
+            } else {
+              const uint32_t w = philox_word(gid, ep, (uint32_t)t, (STREAM_DEMAND << 16) | (uint32_t)(r >> 2), k0,
+                                             k1, r & 3);
+              if (poisson) {
+                cd = p.poisson_draw(w, s_tab);
+              } else {
+                const uint64_t rng = (uint64_t)(p.uniform_high() - p.uniform_low());
+                cd = p.uniform_low() + (int)(((uint64_t)w * rng) >> 32);
+              }
+              if (p.noisy_demand()) {     // IM_div_env.py:246-255: double, then zero
+                const uint32_t wd = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_DOUBLE << 16) | (uint32_t)(r >> 2),
+                                                k0, k1, r & 3);
+                const uint32_t wz = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_ZERO << 16) | (uint32_t)(r >> 2), k0,
+                                                k1, r & 3);
+                if ((uint64_t)wd < A.noisy_demand_thr32) cd = 2 * cd;
+                if ((uint64_t)wz < A.noisy_demand_thr32) cd = 0;
+              }
+            }
+            cust[i] = cd;
+          }
+          const int d = p.delay(i);
+          if (t >= d) arr[i] = s_ring[(p.ring_off(i) + t % d) * BS + tid];
+          if (p.noisy_delay() && t >= d)
+            defer[i] = (uint64_t)philox_word(gid, ep, (uint32_t)t, (STREAM_NOISY_DELAY << 16) | (uint32_t)(i >> 2), k0,
+                                             k1, i & 3) < A.noisy_delay_thr32;
+          // base_stock_policy (base_restock_policy.py:12-20): inv + order_u - backlog at this period,
+          // min(order_max, max(policy - inv_ech, 0)); the env then decodes it like any action
+          const double ie = (double)inv[i] + (double)ou[i] - (double)bl[i];
+          x[i] = fmin((double)p.order_max(i), fmax(lvl[i] - ie, 0.0));
+        }
+      }
+      int order[NT], dem[NT], acq[NT], ship[NT], sto[NT], cout[NT], push[NT];
+      double prof[NT];
+      double rew;
+      bool split_ok;
+      step_core(p, t, x, cust, defer, arr, cin, inv, bl, ou, btoc, order, dem, acq, ship, sto, cout, push, prof,
+                rew, split_ok);
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        if (i < N) {
+          const int d = p.delay(i);
+          s_ring[(p.ring_off(i) + t % d) * BS + tid] = push[i];
+          cin[i] = cout[i];
+        }
+      }
+      if (pass == 0) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+          if (i < N) {
+            inv_s += inv[i];
+            bl_s += bl[i];
+            if (p.retailer_slot(i) >= 0) cbl_s += bl[i];
+          }
+        }
+        ret += rew;
+      }
+      if constexpr (OBJ) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+          const int r = (i < N) ? p.retailer_slot(i) : -1;
+          if (r == pass) {
+            const int k = cust[i];
+            const double w = (k >= 0 && k < pmf_n) ? s_pmf[k] : ((k >= pmf_n && k < A.pmf_len) ? A.pmf[k] : 0.0);
+            const double term = w * rew;
+            const int idx = r * T + t;   // row-major [R][T]: this pass's terms arrive in index order
             if (idx < full) {
               const int j = idx & 7;
 #pragma unroll
@@ -1111,21 +1139,8 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, u
 
   double obj = 0.0;
   if constexpr (OBJ) {
-    if constexpr (LDS_TERMS) {
-      for (int idx = 0; idx < full; ++idx) {
-        const double term = s_terms[idx * BS + tid];
-        const int j = idx & 7;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc8[q] = (q == j) ? acc8[q] + term : acc8[q];
-      }
-      for (int idx = full; idx < n_terms; ++idx) {
-        const double term = s_terms[idx * BS + tid];
-        const int j = idx - full;
-#pragma unroll
-        for (int q = 0; q < 7; ++q) tail[q] = (q == j) ? term : tail[q];
-      }
-    }
-    double sum = (n_terms >= 8) ? pairwise8(acc8) : 0.0;
+    double sum = (n_terms >= 8) ? ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]))
+                                : 0.0;
 #pragma unroll
     for (int q = 0; q < 7; ++q)
       if (q < n_terms - full) sum += tail[q];
@@ -1133,23 +1148,26 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, u
   }
 
   const double v[IMENV_NUM_STATS] = {ret, obj, (double)inv_s, (double)bl_s, (double)cbl_s};
-  const int64_t PS = A.P * A.S;
-  if (valid) {
+  if (A.ep && valid) {
+    const int64_t PS = A.P * A.S;
 #pragma unroll
     for (int m = 0; m < IMENV_NUM_STATS; ++m) A.ep[m * PS + pol * A.S + s] = v[m];
   }
-  // block reduction: wavefront shuffles, then the waves' sums in order through LDS (deterministic)
-  const int lane = tid & 63, wv = tid >> 6;
+  // per-block (sum, M2 about the block mean, count) of every metric
+  const int64_t rem = A.S - sb * BS;
+  const double nb = (double)(rem < BS ? rem : BS);
 #pragma unroll
   for (int m = 0; m < IMENV_NUM_STATS; ++m) {
-    const double w = wave_sum(valid ? v[m] : 0.0);
-    if (lane == 0) s_red[m * (BS / 64) + wv] = w;
-  }
-  __syncthreads();
-  if (tid < IMENV_NUM_STATS) {
-    double acc = 0.0;
-    for (int k = 0; k < BS / 64; ++k) acc += s_red[tid * (BS / 64) + k];
-    A.partial[((int64_t)tid * A.P + pol) * A.bpp + sb] = acc;
+    const double sm = block_sum<BS>(valid ? v[m] : 0.0, s_red);
+    const double mb = sm / nb;
+    const double dv = valid ? v[m] - mb : 0.0;
+    const double m2 = block_sum<BS>(dv * dv, s_red);
+    if (tid == 0) {
+      double* o = A.partial + (((int64_t)m * A.P + pol) * A.bpp + sb) * 3;
+      o[0] = sm;
+      o[1] = m2;
+      o[2] = nb;
+    }
   }
 }
 

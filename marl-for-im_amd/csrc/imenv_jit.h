@@ -61,10 +61,8 @@ struct RolloutFlags {
   bool noisy_delay = false;
   bool noisy_demand = false;  // drawn demand only
   bool objective = false;     // dfo_func objective (pmf given)
-  bool lds_terms = false;     // objective with > 1 retailer: [R][T] products kept in LDS
   uint32_t key() const {
-    return (table ? 1u : 0u) | (noisy_delay ? 2u : 0u) | (noisy_demand ? 4u : 0u) | (objective ? 8u : 0u) |
-           (lds_terms ? 16u : 0u);
+    return (table ? 1u : 0u) | (noisy_delay ? 2u : 0u) | (noisy_demand ? 4u : 0u) | (objective ? 8u : 0u);
   }
 };
 

@@ -55,7 +55,8 @@ void emit2(std::ostream& o, const char* type, const char* name, int n0, int n1, 
 std::string ilit(long long v) { return std::to_string(v); }
 const char* blit(bool b) { return b ? "true" : "false"; }
 
-constexpr int kInlineTable = 64;   // Poisson tables up to this length become a compare-sum
+constexpr int kInlineTable = 64;
+constexpr int kRolloutPmfLds = 256;  // pmf weights staged in LDS (the rest, if any, read from memory)   // Poisson tables up to this length become a compare-sum
 
 // Threads (= envs) per block of the JIT kernel: 256 measured best for the C2 kernel (25.8 us vs
 // 26.3 us at 512 and 27.6 us at 1024, profiles/r01); IMENV_JIT_BS overrides (64..1024, multiple of 64).
@@ -364,12 +365,11 @@ hipError_t jit_launch(const JitKernel& k, hipStream_t st, const SpecDev* sp, con
 }
 
 // ---------------------------------------------------------------- fused base-stock rollout
-int rollout_block_size(const SpecDev& d, const RolloutFlags& f) {
-  // LDS per thread: the in-transit queue (int32 per slot) and, for the multi-retailer objective,
-  // the [R][T] products np.sum needs in index order. Largest block whose LDS fits 64 KiB.
-  const int per = 4 * d.ring_total + (f.lds_terms ? 8 * d.s.num_retailers * d.s.num_periods : 0);
+int rollout_block_size(const SpecDev& d, const RolloutFlags&) {
+  // LDS per block: the in-transit queue (int32 per slot per thread), the Poisson table, the pmf
+  // weights and the reduction scratch. 256 threads unless the queue is long.
   for (int bs : {256, 128, 64})
-    if (bs * per + 4 * IMENV_TABLE_MAX + 8 * IMENV_NUM_STATS * 4 <= 65536) return bs;
+    if (bs * 4 * d.ring_total + 4 * IMENV_TABLE_MAX + 8 * kRolloutPmfLds + 8 * 4 <= 65536) return bs;
   return 0;
 }
 
@@ -380,19 +380,19 @@ std::string jit_rollout_source(const SpecDev& d, int maxc, const RolloutFlags& f
   jf.demand_layout = f.table ? IMENV_LAYOUT_PER_ENV : IMENV_LAYOUT_DRAW;
   std::ostringstream o;
   emit_policy(o, d, maxc, false, jf, bs);
-  const int terms = f.lds_terms ? d.s.num_retailers * d.s.num_periods : 1;
+  const int pmf = f.objective ? kRolloutPmfLds : 1;
   o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
        "imenv_rollout_jit(const imenv::SpecDev* __restrict__ sp, const imenv::RolloutArgs A) {\n"
        "  __shared__ uint32_t s_tab[JitSpec::TAB_LDS];\n"
        "  __shared__ int32_t s_ring[JitSpec::RING * JitSpec::BS];\n"
-       "  __shared__ double s_terms["
-    << terms
-    << " * JitSpec::BS];\n"
-       "  __shared__ double s_red[IMENV_NUM_STATS * (JitSpec::BS / 64)];\n"
+       "  __shared__ double s_pmf["
+    << pmf
+    << "];\n"
+       "  __shared__ double s_red[JitSpec::BS / 64];\n"
        "  const JitSpec p(sp, A);\n"
        "  imenv::rollout_body<JitSpec, "
-    << blit(f.objective) << ", " << blit(f.lds_terms)
-    << ">(p, A, s_tab, s_ring, s_terms, s_red);\n"
+    << blit(f.objective) << ">(p, A, s_tab, s_ring, s_pmf, " << pmf
+    << ", s_red);\n"
        "}\n";
   return o.str();
 }
@@ -401,7 +401,7 @@ bool jit_rollout_load(const SpecDev& d, int maxc, const RolloutFlags& f, const s
                       std::string& msg) {
   const int bs = rollout_block_size(d, f);
   if (bs == 0) {
-    msg = "rollout: in-transit queue + objective terms exceed 64 KiB of LDS at 64 threads per block";
+    msg = "rollout: the in-transit queue exceeds 64 KiB of LDS at 64 threads per block";
     return false;
   }
   const std::string src = jit_rollout_source(d, maxc, f, bs);

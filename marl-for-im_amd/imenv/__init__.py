@@ -8,6 +8,9 @@ imenv_capi.hip; declared in include/imenv.h) driven from Python. Public surface:
   VectorInvEnv(kind, config, n) batched envs on one GPU (vector_env.py)
   InvManagement, MultiAgentInvManagement, InvManagementDiv,
   MultiAgentInvManagementDiv    drop-in single-env adaptors (envs.py)
+  BaseStockRollout, dfo_func, base_stock_policy,
+  optimize_inventory_policy     base-stock policy search on the GPU (policy.py,
+                                base_restock_policy.py's interface)
 
 torch is imported lazily so that the spec builder works without a GPU stack.
 """
@@ -22,4 +25,8 @@ def __getattr__(name):
     if name in ("InvManagement", "MultiAgentInvManagement", "InvManagementDiv", "MultiAgentInvManagementDiv"):
         from . import envs
         return getattr(envs, name)
+    if name in ("BaseStockRollout", "dfo_func", "base_stock_policy", "optimize_inventory_policy",
+                "evaluate_base_stock"):
+        from . import policy
+        return getattr(policy, name)
     raise AttributeError(name)

@@ -69,8 +69,8 @@ def test_jit_specialiser_compiles_every_golden_spec():
 
 def test_jit_rollout_kernel_compiles_for_scalar_reward_specs():
     """hipRTC builds the fused base-stock rollout kernel (rollout_body) for every golden spec with a
-    scalar reward: host demand table + objective (terms in LDS for > 1 retailer), and in-kernel
-    draws + noisy delay (+ noisy demand for the tree specs)."""
+    scalar reward: host demand table + objective (one replay per retailer row for > 1 retailer),
+    and in-kernel draws + noisy delay (+ noisy demand for the tree specs)."""
     from golden_io import case_names, load_case
     from imenv import _native, build_spec
     if not os.path.exists(_native.LIB_PATH):
@@ -83,9 +83,8 @@ def test_jit_rollout_kernel_compiles_for_scalar_reward_specs():
         if hs.reward_mode == _native.REWARD_INDEPENDENT:
             continue
         spec = hs.to_c()
-        lds = 16 if hs.num_retailers > 1 else 0
         nd = 4 if hs.noisy_demand else 0
-        for rk in (1 | 8 | lds, 2 | nd):
+        for rk in (1 | 8, 2 | nd | 8):
             flags = (1 << 12) | (rk << 13)
             rc = lib.imenv_jit_check(ctypes.byref(spec), b"gfx950", flags, log, len(log))
             assert rc == 0, (name, rk, log.value.decode()[:2000])
