@@ -305,6 +305,13 @@ int validate_and_derive(const ImEnvSpec& s, SpecDev& d, int& maxc) {
       p = p * mu / (double)k;
     }
     d.table_len = k;
+    // indexed-search guide (rollout_body's poisson_guided): count of thresholds <= g << (32 - bits)
+    int c = 0;
+    for (int g = 0; g < (1 << IMENV_GUIDE_BITS); ++g) {
+      const uint64_t lo = (uint64_t)g << (32 - IMENV_GUIDE_BITS);
+      while (c < k && (uint64_t)d.table[c] <= lo) ++c;
+      d.guide[g] = (uint16_t)c;
+    }
   } else if (s.demand_dist == IMENV_DEMAND_UNIFORM) {
     if (s.uniform_low >= s.uniform_high)
       return fail(IMENV_E_INVALID, "Lower bound cannot be larger than upper bound");

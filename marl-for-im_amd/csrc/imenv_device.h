@@ -49,6 +49,7 @@ typedef unsigned long long uint64_t;
 #include "imenv.h"
 
 #define IMENV_TABLE_MAX 1024
+#define IMENV_GUIDE_BITS 10
 
 namespace imenv {
 
@@ -66,6 +67,7 @@ struct SpecDev {
   int32_t es;                               // state element bytes: 1 (uint8), 2 (int16) or 4 (int32)
   int32_t table_len;
   uint32_t table[IMENV_TABLE_MAX];          // Poisson inversion thresholds
+  uint16_t guide[1 << IMENV_GUIDE_BITS];    // indexed-search guide: #{thresholds <= g << (32 - bits)}
   // observation lookup: value of group g, node i for raw v in [0, lut_max] at lut[lut_off + v]
   int32_t lut_off[IMENV_NUM_GROUPS][IMENV_MAX_NODES];
   int32_t lut_max[IMENV_NUM_GROUPS][IMENV_MAX_NODES];   // -1: not tabulated
@@ -141,18 +143,39 @@ constexpr uint32_t PH_M0 = 0xD2511F53u, PH_M1 = 0xCD9E8D57u;
 constexpr uint32_t PH_W0 = 0x9E3779B9u, PH_W1 = 0xBB67AE85u;
 constexpr uint32_t STREAM_DEMAND = 0, STREAM_ND_DOUBLE = 1, STREAM_ND_ZERO = 2, STREAM_NOISY_DELAY = 3;
 
-// Philox4x32-10 (Salmon et al. SC'11); oracle/philox.py is the CPU twin.
-__device__ __forceinline__ uint32_t philox_word(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                                uint32_t k0, uint32_t k1, int w) {
+// Philox4x32-10 (Salmon et al. SC'11); oracle/philox.py is the CPU twin. Each round's two 32x32
+// products are taken as 64-bit products (one v_mad_u64_u32 each instead of a mul_lo + mul_hi pair).
+__device__ __forceinline__ uint4 philox4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                         uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     if (r) { k0 += PH_W0; k1 += PH_W1; }
-    const uint32_t hi0 = __umulhi(PH_M0, c0), lo0 = PH_M0 * c0;
-    const uint32_t hi1 = __umulhi(PH_M1, c2), lo1 = PH_M1 * c2;
-    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    const uint64_t p0 = (uint64_t)PH_M0 * c0;
+    const uint64_t p1 = (uint64_t)PH_M1 * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
   }
-  return w == 0 ? c0 : (w == 1 ? c1 : (w == 2 ? c2 : c3));
+  return make_uint4(c0, c1, c2, c3);
+}
+
+__device__ __forceinline__ uint32_t word_of(const uint4& b, int w) {
+  return w == 0 ? b.x : (w == 1 ? b.y : (w == 2 ? b.z : b.w));
+}
+
+// The env's random stream: the 32-bit word for (stream, lane, period t) of env `gid`
+// in episode `ep` is word t mod 4 of Philox(counter = (gid, ep, t / 4, stream << 16 | lane), key =
+// seed). lane = retailer row (demand, noisy demand) or node (noisy delay). One block serves four
+// consecutive periods, so a kernel that runs whole episodes (rollout_body) draws once per 4 periods.
+__device__ __forceinline__ uint4 rng_block(uint32_t gid, uint32_t ep, int t, uint32_t stream, int lane, uint32_t k0,
+                                           uint32_t k1) {
+  return philox4(gid, ep, (uint32_t)t >> 2, (stream << 16) | (uint32_t)lane, k0, k1);
+}
+__device__ __forceinline__ uint32_t rng_word(uint32_t gid, uint32_t ep, int t, uint32_t stream, int lane, uint32_t k0,
+                                             uint32_t k1) {
+  return word_of(rng_block(gid, ep, t, stream, lane, k0, k1), t & 3);
 }
 
 __device__ __forceinline__ int ceil_div_pos(int a, int b) { return (a + b - 1) / b; }
@@ -432,27 +455,19 @@ __device__ __forceinline__ double DynSpec<NT_, MC_, BASE_, ST_>::obs64(int g, in
 }
 
 // ---------------------------------------------------------------- one period of one env
-// The arithmetic of step() on register state (IM_env.py:287-374 and siblings): order decode,
-// demand, arrivals (noisy-delay deferral decided by the caller), shipment, divergent split,
+// The arithmetic of step() on register state (IM_env.py:287-374 and siblings), given the decoded
+// orders: demand, arrivals (noisy-delay deferral decided by the caller), shipment, divergent split,
 // balance equations, profit and reward. inv / bl / ou / btoc are updated in place. Shared by the
 // step kernel (state in HBM rows) and the fused rollout kernel (state in registers, in-transit
 // queue in LDS), so both compute one function.
+// order decode (IM_env.py:298-302; MAIM_env.py:340-347). Division by b - a is replaced by an exact
+// multiply when b - a is a power of two (inv_bma != 0).
 template <class P>
-__device__ __forceinline__ void step_core(const P& p, const int t, const double (&x)[P::NT], const int (&cust)[P::NT],
-                                          const bool (&defer)[P::NT], const int (&arr)[P::NT],
-                                          const int (&cin)[P::NT], int (&inv)[P::NT], int (&bl)[P::NT],
-                                          int (&ou)[P::NT], int (&btoc)[P::NT], int (&order)[P::NT],
-                                          int (&dem)[P::NT], int (&acq)[P::NT], int (&ship)[P::NT],
-                                          int (&sto)[P::NT], int (&cout)[P::NT], int (&push)[P::NT],
-                                          double (&prof)[P::NT], double& rew, bool& split_ok) {
+__device__ __forceinline__ void decode_orders(const P& p, const double (&x)[P::NT], int (&order)[P::NT]) {
   constexpr int NT = P::NT;
-  constexpr int MC = P::MC;
   const int N = p.N();
-  const int T = p.T();
   const double a = p.a();
   const double bma = p.bma();
-  // order decode (IM_env.py:298-302; MAIM_env.py:340-347). Division by b - a is replaced by
-  // an exact multiply when b - a is a power of two (inv_bma != 0).
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     order[i] = 0;
@@ -467,6 +482,20 @@ __device__ __forceinline__ void step_core(const P& p, const int t, const double 
       order[i] = (int)o;
     }
   }
+}
+
+template <class P>
+__device__ __forceinline__ void step_core(const P& p, const int t, const int (&order)[P::NT], const int (&cust)[P::NT],
+                                          const bool (&defer)[P::NT], const int (&arr)[P::NT],
+                                          const int (&cin)[P::NT], int (&inv)[P::NT], int (&bl)[P::NT],
+                                          int (&ou)[P::NT], int (&btoc)[P::NT], int (&dem)[P::NT],
+                                          int (&acq)[P::NT], int (&ship)[P::NT], int (&sto)[P::NT],
+                                          int (&cout)[P::NT], int (&push)[P::NT], double (&prof)[P::NT],
+                                          double& rew, bool& split_ok) {
+  constexpr int NT = P::NT;
+  constexpr int MC = P::MC;
+  const int N = p.N();
+  const int T = p.T();
   // demand (IM_env.py:306-308, IM_div_env.py:380-387)
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
@@ -719,8 +748,7 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
       const int r = p.retailer_slot(i);
       if (r >= 0) {
         if (p.demand_layout() == IMENV_LAYOUT_DRAW) {
-          const uint32_t w = philox_word(gid, ep, (uint32_t)t, (STREAM_DEMAND << 16) | (uint32_t)(r >> 2), k0, k1,
-                                         r & 3);
+          const uint32_t w = rng_word(gid, ep, t, STREAM_DEMAND, r, k0, k1);
           if (poisson) {
             cdraw[i] = p.poisson_draw(w, s_tab);
           } else {
@@ -729,17 +757,14 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           }
         }
         if (p.noisy_demand()) {
-          const uint32_t wd = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_DOUBLE << 16) | (uint32_t)(r >> 2), k0, k1,
-                                          r & 3);
-          const uint32_t wz = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_ZERO << 16) | (uint32_t)(r >> 2), k0, k1,
-                                          r & 3);
+          const uint32_t wd = rng_word(gid, ep, t, STREAM_ND_DOUBLE, r, k0, k1);
+          const uint32_t wz = rng_word(gid, ep, t, STREAM_ND_ZERO, r, k0, k1);
           nd_double[i] = (uint64_t)wd < A.noisy_demand_thr32;
           nd_zero[i] = (uint64_t)wz < A.noisy_demand_thr32;
         }
       }
       if (p.noisy_delay() && !p.has_delay_u() && t >= p.delay(i))
-        nd_delay[i] = (uint64_t)philox_word(gid, ep, (uint32_t)t, (STREAM_NOISY_DELAY << 16) | (uint32_t)(i >> 2), k0,
-                                            k1, i & 3) < A.noisy_delay_thr32;
+        nd_delay[i] = (uint64_t)rng_word(gid, ep, t, STREAM_NOISY_DELAY, i, k0, k1) < A.noisy_delay_thr32;
     }
   }
 
@@ -797,7 +822,8 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   double prof[NT];
   double rew;
   bool split_ok;
-  step_core(p, t, x, cust, defer, arr, cin, inv, bl, ou, btoc, order, dem, acq, ship, sto, cout, push, prof, rew,
+  decode_orders(p, x, order);
+  step_core(p, t, order, cust, defer, arr, cin, inv, bl, ou, btoc, dem, acq, ship, sto, cout, push, prof, rew,
             split_ok);
 
   // ================= (C) stores
@@ -964,6 +990,15 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
 // Each block (one policy, BS scenarios) then reduces every metric with wavefront shuffles + LDS to
 // (sum, M2 about the block mean, count): the stats kernel merges blocks with Chan's pairwise update
 // (stable, deterministic).
+// Poisson inversion by an indexed search (Chen & Asau): guide[g] = #{thresholds <= g * 2^22}, then a
+// short scan; equals the compare-and-count of poisson_draw (searchsorted right) for every w.
+__device__ __forceinline__ int poisson_guided(uint32_t w, const uint32_t* __restrict__ thr,
+                                              const uint16_t* __restrict__ guide, int len) {
+  int k = guide[w >> (32 - IMENV_GUIDE_BITS)];
+  while (k < len && w >= thr[k]) ++k;
+  return k;
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -986,8 +1021,9 @@ __device__ __forceinline__ double block_sum(double v, double* s_red) {
 }
 
 template <class P, bool OBJ>
-__device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, uint32_t* s_tab, int32_t* s_ring,
-                                             double* s_pmf, int pmf_lds, double* s_red) {
+__device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, const SpecDev* __restrict__ sp,
+                                             uint32_t* s_thr, uint16_t* s_guide, int32_t* s_ring, double* s_pmf,
+                                             int pmf_lds, double* s_red) {
   constexpr int NT = P::NT;
   constexpr int BS = P::BS;
   const int tid = threadIdx.x;
@@ -1003,14 +1039,18 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, u
   const uint32_t ep = A.episode;
   const uint64_t seed = p.seed();
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-  const bool draw = A.demand == nullptr;
+  const bool draw = p.demand_layout() == IMENV_LAYOUT_DRAW;   // JIT flag: no table
   const bool poisson = draw && p.demand_dist() == IMENV_DEMAND_POISSON;
-  p.stage_tables(s_tab, poisson);
+  const int n_thr = sp->table_len;
+  if (poisson) {
+    for (int k = tid; k < n_thr; k += BS) s_thr[k] = sp->table[k];
+    for (int k = tid; k < (1 << IMENV_GUIDE_BITS); k += BS) s_guide[k] = sp->guide[k];
+  }
   const int pmf_n = A.pmf_len < pmf_lds ? A.pmf_len : pmf_lds;
   if constexpr (OBJ) {
     for (int k = tid; k < pmf_n; k += BS) s_pmf[k] = A.pmf[k];
-    __syncthreads();
   }
+  __syncthreads();
 
   double lvl[NT];
 #pragma unroll
@@ -1040,9 +1080,29 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, u
       if (i < N)
         for (int k = 0; k < p.delay(i); ++k) s_ring[(p.ring_off(i) + k) * BS + tid] = 0;
 
+    uint4 rb_dem[NT], rb_dbl[NT], rb_zero[NT], rb_delay[NT];   // one Philox block per 4 periods
 #pragma unroll 1
     for (int t = 0; t < T; ++t) {
-      int cust[NT], arr[NT];
+      const int tw = t & 3;
+      if (tw == 0 && draw) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+          const int r = (i < N) ? p.retailer_slot(i) : -1;
+          if (r >= 0) {
+            rb_dem[i] = rng_block(gid, ep, t, STREAM_DEMAND, r, k0, k1);
+            if (p.noisy_demand()) {
+              rb_dbl[i] = rng_block(gid, ep, t, STREAM_ND_DOUBLE, r, k0, k1);
+              rb_zero[i] = rng_block(gid, ep, t, STREAM_ND_ZERO, r, k0, k1);
+            }
+          }
+        }
+      }
+      if (tw == 0 && p.noisy_delay()) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+          if (i < N) rb_delay[i] = rng_block(gid, ep, t, STREAM_NOISY_DELAY, i, k0, k1);
+      }
+      int cust[NT], arr[NT], order[NT];
       bool defer[NT];
       double x[NT];
 #pragma unroll
@@ -1051,6 +1111,7 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, u
         defer[i] = false;
         arr[i] = 0;
         x[i] = 0.0;
+        order[i] = 0;
         if (i < N) {
           const int r = p.retailer_slot(i);
           if (r >= 0) {
@@ -1058,41 +1119,38 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, u
             if (!draw) {
               cd = A.demand[((int64_t)t * R + r) * A.S + sl];
             } else {
-              const uint32_t w = philox_word(gid, ep, (uint32_t)t, (STREAM_DEMAND << 16) | (uint32_t)(r >> 2), k0,
-                                             k1, r & 3);
+              const uint32_t w = word_of(rb_dem[i], tw);
               if (poisson) {
-                cd = p.poisson_draw(w, s_tab);
+                cd = poisson_guided(w, s_thr, s_guide, n_thr);
               } else {
                 const uint64_t rng = (uint64_t)(p.uniform_high() - p.uniform_low());
                 cd = p.uniform_low() + (int)(((uint64_t)w * rng) >> 32);
               }
               if (p.noisy_demand()) {     // IM_div_env.py:246-255: double, then zero
-                const uint32_t wd = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_DOUBLE << 16) | (uint32_t)(r >> 2),
-                                                k0, k1, r & 3);
-                const uint32_t wz = philox_word(gid, ep, (uint32_t)t, (STREAM_ND_ZERO << 16) | (uint32_t)(r >> 2), k0,
-                                                k1, r & 3);
-                if ((uint64_t)wd < A.noisy_demand_thr32) cd = 2 * cd;
-                if ((uint64_t)wz < A.noisy_demand_thr32) cd = 0;
+                if ((uint64_t)word_of(rb_dbl[i], tw) < A.noisy_demand_thr32) cd = 2 * cd;
+                if ((uint64_t)word_of(rb_zero[i], tw) < A.noisy_demand_thr32) cd = 0;
               }
             }
             cust[i] = cd;
           }
           const int d = p.delay(i);
           if (t >= d) arr[i] = s_ring[(p.ring_off(i) + t % d) * BS + tid];
-          if (p.noisy_delay() && t >= d)
-            defer[i] = (uint64_t)philox_word(gid, ep, (uint32_t)t, (STREAM_NOISY_DELAY << 16) | (uint32_t)(i >> 2), k0,
-                                             k1, i & 3) < A.noisy_delay_thr32;
-          // base_stock_policy (base_restock_policy.py:12-20): inv + order_u - backlog at this period,
-          // min(order_max, max(policy - inv_ech, 0)); the env then decodes it like any action
-          const double ie = (double)inv[i] + (double)ou[i] - (double)bl[i];
-          x[i] = fmin((double)p.order_max(i), fmax(lvl[i] - ie, 0.0));
+          if (p.noisy_delay() && t >= d) defer[i] = (uint64_t)word_of(rb_delay[i], tw) < A.noisy_delay_thr32;
+          // base_stock_policy (base_restock_policy.py:12-20): order up to lvl from the echelon position
+          // inv + order_u - backlog (integers: exact, as the reference's float64 sum of integers),
+          // min(order_max, max(policy - position, 0)); then the env's decode
+          const double om = (double)p.order_max(i);
+          const double xa = fmin(om, fmax(lvl[i] - (double)(inv[i] + ou[i] - bl[i]), 0.0));
+          if (p.std_actions()) x[i] = xa;
+          else order[i] = (int)rint(xa);   // unstandardised: the decode's clip is a no-op on [0, om]
         }
       }
-      int order[NT], dem[NT], acq[NT], ship[NT], sto[NT], cout[NT], push[NT];
+      if (p.std_actions()) decode_orders(p, x, order);
+      int dem[NT], acq[NT], ship[NT], sto[NT], cout[NT], push[NT];
       double prof[NT];
       double rew;
       bool split_ok;
-      step_core(p, t, x, cust, defer, arr, cin, inv, bl, ou, btoc, order, dem, acq, ship, sto, cout, push, prof,
+      step_core(p, t, order, cust, defer, arr, cin, inv, bl, ou, btoc, dem, acq, ship, sto, cout, push, prof,
                 rew, split_ok);
 #pragma unroll
       for (int i = 0; i < NT; ++i) {

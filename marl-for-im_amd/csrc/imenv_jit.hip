@@ -369,7 +369,8 @@ int rollout_block_size(const SpecDev& d, const RolloutFlags&) {
   // LDS per block: the in-transit queue (int32 per slot per thread), the Poisson table, the pmf
   // weights and the reduction scratch. 256 threads unless the queue is long.
   for (int bs : {256, 128, 64})
-    if (bs * 4 * d.ring_total + 4 * IMENV_TABLE_MAX + 8 * kRolloutPmfLds + 8 * 4 <= 65536) return bs;
+    if (bs * 4 * d.ring_total + 4 * IMENV_TABLE_MAX + 2 * (1 << IMENV_GUIDE_BITS) + 8 * kRolloutPmfLds + 8 * 4 <= 65536)
+      return bs;
   return 0;
 }
 
@@ -383,7 +384,12 @@ std::string jit_rollout_source(const SpecDev& d, int maxc, const RolloutFlags& f
   const int pmf = f.objective ? kRolloutPmfLds : 1;
   o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
        "imenv_rollout_jit(const imenv::SpecDev* __restrict__ sp, const imenv::RolloutArgs A) {\n"
-       "  __shared__ uint32_t s_tab[JitSpec::TAB_LDS];\n"
+       "  __shared__ uint32_t s_thr["
+    << (d.s.demand_dist == IMENV_DEMAND_POISSON && !f.table ? IMENV_TABLE_MAX : 1)
+    << "];\n"
+       "  __shared__ uint16_t s_guide["
+    << (d.s.demand_dist == IMENV_DEMAND_POISSON && !f.table ? (1 << IMENV_GUIDE_BITS) : 1)
+    << "];\n"
        "  __shared__ int32_t s_ring[JitSpec::RING * JitSpec::BS];\n"
        "  __shared__ double s_pmf["
     << pmf
@@ -391,7 +397,7 @@ std::string jit_rollout_source(const SpecDev& d, int maxc, const RolloutFlags& f
        "  __shared__ double s_red[JitSpec::BS / 64];\n"
        "  const JitSpec p(sp, A);\n"
        "  imenv::rollout_body<JitSpec, "
-    << blit(f.objective) << ">(p, A, s_tab, s_ring, s_pmf, " << pmf
+    << blit(f.objective) << ">(p, A, sp, s_thr, s_guide, s_ring, s_pmf, " << pmf
     << ", s_red);\n"
        "}\n";
   return o.str();

@@ -2,7 +2,7 @@
 
 TEST INFRASTRUCTURE ONLY (see oracle/__init__.py). The product draws the same
 numbers inside the HIP step kernel (marl-for-im_amd/csrc/imenv_device.h,
-``philox_word`` and the demand block of ``step_body``); this module lets the tests check those
+``rng_word`` / ``rng_block`` in ``step_body`` and ``rollout_body``); this module lets the tests check those
 in-kernel draws bit-exactly on the CPU.
 
 Why this exists: the reference draws the whole demand horizon at ``reset()`` from
@@ -18,7 +18,9 @@ Random123 ``philox4x32_R(10, ...)``), pinned by the published known-answer vecto
 in tests/test_oracle_golden.py (KAT tests).
 
 Counter layout used by the product (all uint32):
-    c0 = global env id, c1 = episode, c2 = period t, c3 = (stream << 16) | block
+    c0 = global env id, c1 = episode, c2 = period t // 4, c3 = (stream << 16) | lane
+and the word for period t is output word t % 4, so one Philox block serves four consecutive
+periods (lane = retailer row for demand draws, node for noisy delay).
 Key: (seed & 0xffffffff, seed >> 32).
 """
 import numpy as np
@@ -29,7 +31,7 @@ W0 = np.uint32(0x9E3779B9)
 W1 = np.uint32(0xBB67AE85)
 MASK32 = np.uint64(0xFFFFFFFF)
 
-# Stream ids (counter word c3 high half); must match imenv_kernels.hip.
+# Stream ids (counter word c3 high half); must match imenv_device.h.
 STREAM_DEMAND = 0
 STREAM_NOISY_DEMAND_DOUBLE = 1
 STREAM_NOISY_DEMAND_ZERO = 2
@@ -60,6 +62,12 @@ def philox4x32_10(c0, c1, c2, c3, k0, k1):
         c0, c1, c2, c3 = n0, n1, n2, n3
     return (c0.astype(np.uint32), c1.astype(np.uint32),
             c2.astype(np.uint32), c3.astype(np.uint32))
+
+
+def stream_word(gid, ep, t, stream, lane, k0, k1):
+    """The product's random word for (stream, lane, period t): word t % 4 of the Philox block with
+    counter (gid, ep, t // 4, stream << 16 | lane) (imenv_device.h rng_word)."""
+    return philox4x32_10(gid, ep, int(t) >> 2, (int(stream) << 16) | int(lane), k0, k1)[int(t) & 3]
 
 
 def split_seed(seed):
