@@ -253,6 +253,26 @@ int imenv_step(ImEnv* env, const void* actions, int action_dtype, void* obs, int
  * device and kernel cache. Always runs a hipRTC-specialised kernel (IMENV_E_UNSUPPORTED without it). */
 int imenv_base_stock_rollout(ImEnv* env, const ImEnvRollout* args, void* stream);
 
+/* Evaluation-harness metrics (inv_management.py:567-606, MA_inv_management.py:517-587,
+ * MA_inv_management_div.py): with a buffer attached, every step() adds, per env, into row e of
+ * acc (device double [n][4 + N], caller-owned; period 0 restarts each row from zero):
+ *   [0] episode reward: += reward (IM / IM_div), or += each agent's reward in agent order (MA)
+ *   [1] total inventory: += sum over agents of rev_scale(obs[m][0], 0, inv_max[m], a, b)
+ *   [2] total backlog:   += sum over agents of rev_scale(obs[m][1], 0, inv_max[m], a, b)
+ *   [3] customer backlog: += rev_scale(obs[0][1], 0, inv_max[0], a, b)
+ *   [4 + m] stage reward: += profit[m]
+ * from the float64 observation, in the harness's own summation order. NULL detaches. */
+#define IMENV_METRIC_RETURN 0
+#define IMENV_METRIC_INVENTORY 1
+#define IMENV_METRIC_BACKLOG 2
+#define IMENV_METRIC_CUSTOMER_BACKLOG 3
+#define IMENV_METRIC_STAGE_PROFIT 4
+int imenv_set_episode_metrics(ImEnv* env, double* acc);
+
+/* np.mean / np.std (population) of each column of a device float64 [rows][cols] matrix into
+ * out (device double [cols][2]) — e.g. the harness metrics above over n test episodes. */
+int imenv_column_stats(const double* x, int64_t rows, int32_t cols, double* out, void* stream);
+
 /* State the reference's callers read directly (base_restock_policy.py:12:
  * env.inv/order_u/backlog[env.period]). Copies int32 [N][n] SoA into the given
  * device buffers (any may be NULL); *period (HOST) receives the current period. */
@@ -298,7 +318,7 @@ int imenv_kernel_info(const ImEnv* env, char* buf, int64_t len);
 
 /* Diagnostics (no device needed): generate and compile with hipRTC the specialised step kernel of
  * `spec` for `arch` (e.g. "gfx950"); flags = bit0 f64 actions, bit1 f64 obs, bit2 noisy delay,
- * bit3 noisy demand, bit4 host-fed delay uniforms, bits 5-11 demand layout. With bit 12 set it
+ * bit3 noisy demand, bit4 host-fed delay uniforms, bits 5-9 demand layout, bit10 episode metrics. With bit 12 set it
  * compiles the base-stock rollout kernel instead: bit13 demand table, bit14 noisy delay, bit15 noisy
  * demand, bit16 objective. `log` receives "ok" or
  * the compiler log. */

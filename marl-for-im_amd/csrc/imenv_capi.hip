@@ -102,6 +102,37 @@ __global__ void __launch_bounds__(256) imenv_rollout_stats_kernel(const double* 
   }
 }
 
+// np.mean / np.std (population) of every column of a row-major [rows][cols] float64 matrix: one block
+// per column, the two-pass form np.std uses (mean, then the mean of squared deviations); strided
+// per-thread sums, wavefront shuffles and a fixed wave order (deterministic).
+__global__ void __launch_bounds__(256) imenv_column_stats_kernel(const double* __restrict__ x, int64_t rows,
+                                                                 int32_t cols, double* __restrict__ out) {
+  __shared__ double s_w[4];
+  const int c = blockIdx.x;
+  const int tid = threadIdx.x;
+  auto block_sum = [&](double v) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((tid & 63) == 0) s_w[tid >> 6] = v;
+    __syncthreads();
+    const double r = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);
+    __syncthreads();
+    return r;
+  };
+  double a = 0.0;
+  for (int64_t r = tid; r < rows; r += 256) a += x[r * cols + c];
+  const double mean = block_sum(a) / (double)rows;
+  double q = 0.0;
+  for (int64_t r = tid; r < rows; r += 256) {
+    const double d = x[r * cols + c] - mean;
+    q += d * d;
+  }
+  const double var = block_sum(q) / (double)rows;
+  if (tid == 0) {
+    out[2 * c] = mean;
+    out[2 * c + 1] = sqrt(var);
+  }
+}
+
 thread_local std::string g_err;
 
 int fail(int code, const std::string& msg) {
@@ -382,6 +413,7 @@ struct ImEnv {
   double* d_roll_part = nullptr;
   size_t roll_part_cap = 0;
   std::string last_rollout;
+  double* d_metrics = nullptr;   // caller-owned [n][4 + N] (imenv_set_episode_metrics)
 };
 
 extern "C" {
@@ -546,6 +578,7 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
   A.lut32 = h->d_lut32;
   A.lut64 = h->d_lut64;
   A.episode = h->d_episode;
+  A.metrics = h->d_metrics;
   A.n = h->n;
   A.env_offset = (uint32_t)h->env_offset;
   A.t = h->t;
@@ -573,6 +606,7 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
     f.noisy_demand = A.noisy_demand != 0;
     f.has_delay_u = A.delay_u != nullptr;
     f.demand_layout = A.demand_layout;
+    f.metrics = A.metrics != nullptr;
     auto it = h->jit_k.find(f.key());
     if (it == h->jit_k.end()) {
       // compiling + loading a module is not stream work: never do it while the stream is being
@@ -692,6 +726,21 @@ int imenv_base_stock_rollout(ImEnv* h, const ImEnvRollout* r, void* stream) {
                        h->d_roll_part, r->policy_stats, P, S, bpp);
     HIPCHK(hipGetLastError());
   }
+  return IMENV_OK;
+}
+
+int imenv_set_episode_metrics(ImEnv* h, double* acc) {
+  if (!h) return fail(IMENV_E_INVALID, "null handle");
+  h->d_metrics = acc;
+  return IMENV_OK;
+}
+
+int imenv_column_stats(const double* x, int64_t rows, int32_t cols, double* out, void* stream) {
+  if (!x || !out) return fail(IMENV_E_INVALID, "null argument");
+  if (rows < 1 || cols < 1 || cols > 65535) return fail(IMENV_E_INVALID, "rows >= 1 and 1 <= cols <= 65535");
+  hipLaunchKernelGGL(imenv_column_stats_kernel, dim3((unsigned)cols), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     x, rows, cols, out);
+  HIPCHK(hipGetLastError());
   return IMENV_OK;
 }
 
@@ -836,7 +885,8 @@ int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, cha
   f.noisy_delay = flags & 4u;
   f.noisy_demand = flags & 8u;
   f.has_delay_u = flags & 16u;
-  f.demand_layout = (int)(flags >> 5);
+  f.metrics = flags & 1024u;
+  f.demand_layout = (int)((flags >> 5) & 31u);
   std::string msg;
   std::string src;
   if (flags & (1u << 12)) {   // the base-stock rollout kernel; bits 13..17 = RolloutFlags::key()

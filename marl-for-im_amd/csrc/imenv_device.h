@@ -104,6 +104,7 @@ struct StepArgs {
   const float* lut32;
   const double* lut64;
   const uint32_t* episode;    // device word written by the reset kernel (graph-replay safe)
+  double* metrics;            // [n][4 + N] evaluation-harness accumulators (imenv_set_episode_metrics) or null
   int64_t n;
   uint32_t env_offset;
   int32_t t;
@@ -408,6 +409,7 @@ struct DynSpec {
   __device__ bool noisy_demand() const { return A.noisy_demand != 0; }
   __device__ bool has_delay_u() const { return A.delay_u != nullptr; }
   __device__ bool uses_hist() const { return A.hist_d != nullptr; }
+  __device__ bool has_metrics() const { return A.metrics != nullptr; }
   // observation value of group g, node i for raw value v (table lookup, see obs_value32)
   __device__ float obs32(int g, int i, int v, const float* __restrict__ lut) const;
   __device__ double obs64(int g, int i, int v, const double* __restrict__ lut) const;
@@ -681,6 +683,9 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   ST r_arr[NT];
   int cdem[NT];
   double du[NT];
+  double macc[4 + NT];
+#pragma unroll
+  for (int k = 0; k < 4 + NT; ++k) macc[k] = 0.0;
 #pragma unroll
   for (int q = 0; q < 2 * NT; ++q) aw[q] = 0;
 #pragma unroll
@@ -732,6 +737,10 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
     if (p.has_delay_u()) {
 #pragma unroll
       for (int i = 0; i < NT; ++i) if (i < N) du[i] = A.delay_u[((int64_t)t * N + i) * n + el];
+    }
+    if (p.has_metrics() && t > 0) {   // period 0 starts the episode's sums from zero
+#pragma unroll
+      for (int k = 0; k < 4 + NT; ++k) if (k < 4 + N) macc[k] = A.metrics[el * (4 + N) + k];
     }
   }
   p.stage_tables(s_tab, poisson);
@@ -850,6 +859,40 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
       for (int i = 0; i < NT; ++i) if (i < N) A.reward[e * N + i] = prof[i];
     } else {
       A.reward[e] = rew;
+    }
+    if (p.has_metrics()) {
+      // the reference's evaluation harness, per env (inv_management.py:586-597, MA_inv_management.py:559-572,
+      // MA_inv_management_div.py:540-553): episode_reward += reward (each agent's, in agent order, for
+      // the multi-agent envs); per step, the sum over agents of rev_scale(obs[m][0 | 1], 0, inv_max[m], a, b)
+      // from the float64 observation; customer backlog from agent 0's; stage_rewards[m] += profit[m]
+      const double a = p.a(), bma = p.bma();
+      double r0 = macc[0];
+      if (p.reward_mode() == IMENV_REWARD_SUM) {
+        r0 += rew;
+      } else {
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+          if (i < N) r0 += (p.reward_mode() == IMENV_REWARD_SHARED_MEAN) ? rew : prof[i];
+      }
+      double si = 0.0, sb = 0.0, c0 = 0.0;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        if (i < N) {
+          const double im = (double)p.inv_max(i) - 0.0;
+          const double ri = ((p.obs64(IMENV_G_INV, i, inv[i], A.lut64) - a) * im) / bma + 0.0;
+          const double rb = ((p.obs64(IMENV_G_BACKLOG, i, bl[i], A.lut64) - a) * im) / bma + 0.0;
+          si += ri;
+          sb += rb;
+          if (i == 0) c0 = rb;
+        }
+      }
+      double* row = A.metrics + e * (4 + N);
+      row[0] = r0;
+      row[1] = macc[1] + si;
+      row[2] = macc[2] + sb;
+      row[3] = macc[3] + c0;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) if (i < N) row[4 + i] = macc[4 + i] + prof[i];
     }
     if (A.i_order) {   // info (IM_env.py:345-350)
 #pragma unroll

@@ -188,6 +188,7 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
   sc("bool", "noisy_demand", blit(f.noisy_demand));
   sc("bool", "has_delay_u", blit(f.has_delay_u));
   sc("bool", "uses_hist", blit(uses_hist));
+  sc("bool", "has_metrics", blit(f.metrics));
   auto I = [](const int32_t* a) { return [a](int i) { return ilit(a[i]); }; };
   auto Dd = [](const double* a) { return [a](int i) { return dlit(a[i]); }; };
   emit1(o, "int", "delay", N, I(s.delay), "1");

@@ -31,6 +31,7 @@ F32, F64 = 0, 1
 STAT_RETURN, STAT_OBJECTIVE, STAT_INVENTORY, STAT_BACKLOG, STAT_CUSTOMER_BACKLOG = range(5)
 NUM_STATS = 5
 STAT_NAMES = ("return", "objective", "inventory", "backlog", "customer_backlog")
+METRIC_NAMES = ("episode_reward", "total_inventory", "total_backlog", "customer_backlog")   # + stage_reward[N]
 
 
 class ImEnvNativeError(RuntimeError):
@@ -78,6 +79,8 @@ SYMBOLS = [
     ("imenv_step", c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, POINTER(ImEnvInfo),
                            POINTER(c_int32), c_void_p]),
     ("imenv_base_stock_rollout", c_int, [c_void_p, POINTER(ImEnvRollout), c_void_p]),
+    ("imenv_set_episode_metrics", c_int, [c_void_p, c_void_p]),
+    ("imenv_column_stats", c_int, [c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
     ("imenv_get_state", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_int32), c_void_p]),
     ("imenv_get_errors", c_int, [c_void_p, c_void_p, POINTER(c_uint32), c_void_p]),
     ("imenv_dims", c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),

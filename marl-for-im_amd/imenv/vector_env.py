@@ -179,6 +179,36 @@ class VectorInvEnv:
                   "imenv_get_errors")
         return flags, int(anyv.value)
 
+    def attach_metrics(self, enable=True):
+        """Accumulate the reference evaluation harness's per-episode metrics in every step()
+        (imenv_set_episode_metrics): episode reward, total inventory / backlog, customer backlog and
+        per-stage reward, per env, as inv_management.py:567-606 / MA_inv_management.py:517-587 do."""
+        if enable:
+            self._metrics = torch.zeros((self.n, 4 + self.N), dtype=torch.float64, device=self.device)
+            ptr = self._metrics.data_ptr()
+        else:
+            self._metrics, ptr = None, None
+        nat.check(self.lib.imenv_set_episode_metrics(self._h, ptr), "imenv_set_episode_metrics")
+
+    def metrics(self):
+        """Per-env sums since the last reset: {name: [n]} plus "stage_reward" [n, N] (device tensors)."""
+        m = getattr(self, "_metrics", None)
+        if m is None:
+            raise RuntimeError("attach_metrics() first")
+        out = {k: m[:, j] for j, k in enumerate(nat.METRIC_NAMES)}
+        out["stage_reward"] = m[:, 4:]
+        return out
+
+    def metrics_stats(self):
+        """np.mean / np.std over the n envs of every metric column: [4 + N, 2] (imenv_column_stats)."""
+        m = getattr(self, "_metrics", None)
+        if m is None:
+            raise RuntimeError("attach_metrics() first")
+        out = torch.empty((m.shape[1], 2), dtype=torch.float64, device=self.device)
+        nat.check(self.lib.imenv_column_stats(m.data_ptr(), m.shape[0], m.shape[1], out.data_ptr(), self._stream()),
+                  "imenv_column_stats")
+        return out
+
     def poisson_table(self):
         ln = c_int32()
         nat.check(self.lib.imenv_poisson_table(self._h, None, 0, byref(ln)), "imenv_poisson_table")

@@ -52,7 +52,7 @@ def test_missing_library_fails_loudly(tmp_path):
 def test_jit_specialiser_compiles_every_golden_spec():
     """hipRTC builds the spec-specialised step kernel for every golden config (no device needed),
     for the bench's call flags (f32 actions/obs, in-kernel draws) and the parity-test flags
-    (f64 actions/obs, per-env demand table, host-fed delay uniforms)."""
+    (f64 actions/obs, per-env demand table, host-fed delay uniforms, harness metrics)."""
     from golden_io import case_names, load_case
     from imenv import _native, build_spec
     if not os.path.exists(_native.LIB_PATH):
@@ -62,7 +62,7 @@ def test_jit_specialiser_compiles_every_golden_spec():
     for name in case_names():
         meta, _ = load_case(name)
         spec = build_spec(meta["kind"], meta["config"]).to_c()
-        for flags in (0, 1 | 2 | (_native.LAYOUT_PER_ENV << 5) | (16 if meta["noisy"] else 0)):
+        for flags in (0, 1 | 2 | (_native.LAYOUT_PER_ENV << 5) | (16 if meta["noisy"] else 0) | 1024):
             rc = lib.imenv_jit_check(ctypes.byref(spec), b"gfx950", flags, log, len(log))
             assert rc == 0, (name, flags, log.value.decode()[:2000])
 
