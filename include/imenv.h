@@ -273,6 +273,19 @@ int imenv_set_episode_metrics(ImEnv* env, double* acc);
  * out (device double [cols][2]) — e.g. the harness metrics above over n test episodes. */
 int imenv_column_stats(const double* x, int64_t rows, int32_t cols, double* out, void* stream);
 
+/* Centralised-critic observations: replaces central_critic_observer (models/CC_Model.py:196-214)
+ * plus the opponent actions FillInActions writes (:165-193; CC_inv_management.py:394-407 in the
+ * evaluation loop), flattened in RLlib's order for the Dict space of CC_inv_management.py:137-141
+ * (keys sorted: opponent_action, opponent_obs, own_obs). For rows = n envs x num_agents agents:
+ *   out[e][m] = [clip(actions[e][o], clip_lo, clip_hi) for o != m]
+ *               [obs[e][o][0:F] for o != m] [obs[e][m][0:F]]        (o ascending)
+ * obs: device [n][N][F] (obs_dtype), actions: device [n][N] (action_dtype) or NULL (zeros, as
+ * central_critic_observer leaves them), out: device [n][N][N*F + N - 1] (obs_dtype). Works on any
+ * row batch (e.g. a [T*n] rollout buffer); no env handle needed. */
+int imenv_cc_observation(int64_t n, int32_t num_agents, int32_t num_features, const void* obs, int obs_dtype,
+                         const void* actions, int action_dtype, double clip_lo, double clip_hi, void* out,
+                         void* stream);
+
 /* State the reference's callers read directly (base_restock_policy.py:12:
  * env.inv/order_u/backlog[env.period]). Copies int32 [N][n] SoA into the given
  * device buffers (any may be NULL); *period (HOST) receives the current period. */

@@ -133,6 +133,42 @@ __global__ void __launch_bounds__(256) imenv_column_stats_kernel(const double* _
   }
 }
 
+// Centralised-critic observations (models/CC_Model.py:196-214 central_critic_observer + :165-193
+// FillInActions), flattened the way RLlib flattens the Dict space {own_obs, opponent_obs,
+// opponent_action} for the value model (gym sorts Dict keys): per env e and agent m, a row of
+// N*F + N - 1 values
+//   [ clip(action[o], lo, hi) for o != m ][ obs[o][:] for o != m ][ obs[m][:] ]
+// (o in agent order). One thread per output element: the writes are one contiguous stream, the
+// reads gather from the env's own [N][F] obs row and [N] action row (cache-resident).
+template <typename OT, typename AT>
+__global__ void __launch_bounds__(256) imenv_cc_obs_kernel(const OT* __restrict__ obs, const AT* __restrict__ act,
+                                                           int64_t n, int N, int F, double lo, double hi,
+                                                           OT* __restrict__ out) {
+  const int Fcc = N * F + N - 1;
+  const int64_t per_env = (int64_t)N * Fcc;
+  const int64_t total = n * per_env;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += stride) {
+    const int64_t e = q / per_env;
+    const int r = (int)(q - e * per_env);
+    const int m = r / Fcc;
+    const int j = r - m * Fcc;
+    OT v;
+    if (j < N - 1) {                          // opponent_action
+      const int o = j < m ? j : j + 1;
+      v = act ? (OT)fmin(fmax((double)act[e * N + o], lo), hi) : (OT)0;
+    } else if (j < (N - 1) * (F + 1)) {       // opponent_obs
+      const int k = j - (N - 1);
+      const int oi = k / F;
+      const int o = oi < m ? oi : oi + 1;
+      v = obs[(e * N + o) * F + (k - oi * F)];
+    } else {                                  // own_obs
+      v = obs[(e * N + m) * F + (j - (N - 1) * (F + 1))];
+    }
+    out[q] = v;
+  }
+}
+
 thread_local std::string g_err;
 
 int fail(int code, const std::string& msg) {
@@ -740,6 +776,38 @@ int imenv_column_stats(const double* x, int64_t rows, int32_t cols, double* out,
   if (rows < 1 || cols < 1 || cols > 65535) return fail(IMENV_E_INVALID, "rows >= 1 and 1 <= cols <= 65535");
   hipLaunchKernelGGL(imenv_column_stats_kernel, dim3((unsigned)cols), dim3(256), 0, static_cast<hipStream_t>(stream),
                      x, rows, cols, out);
+  HIPCHK(hipGetLastError());
+  return IMENV_OK;
+}
+
+int imenv_cc_observation(int64_t n, int32_t num_agents, int32_t num_features, const void* obs, int obs_dtype,
+                         const void* actions, int action_dtype, double clip_lo, double clip_hi, void* out,
+                         void* stream) {
+  if (!obs || !out) return fail(IMENV_E_INVALID, "null argument");
+  if (n < 1 || num_agents < 2 || num_features < 1) return fail(IMENV_E_INVALID, "n >= 1, num_agents >= 2, F >= 1");
+  if ((obs_dtype != IMENV_F32 && obs_dtype != IMENV_F64) || (action_dtype != IMENV_F32 && action_dtype != IMENV_F64))
+    return fail(IMENV_E_INVALID, "bad dtype");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int64_t total = n * num_agents * (int64_t)(num_agents * num_features + num_agents - 1);
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  const dim3 g((unsigned)blocks), b(256);
+  if (obs_dtype == IMENV_F32 && action_dtype == IMENV_F32)
+    hipLaunchKernelGGL((imenv_cc_obs_kernel<float, float>), g, b, 0, st, static_cast<const float*>(obs),
+                       static_cast<const float*>(actions), n, num_agents, num_features, clip_lo, clip_hi,
+                       static_cast<float*>(out));
+  else if (obs_dtype == IMENV_F32)
+    hipLaunchKernelGGL((imenv_cc_obs_kernel<float, double>), g, b, 0, st, static_cast<const float*>(obs),
+                       static_cast<const double*>(actions), n, num_agents, num_features, clip_lo, clip_hi,
+                       static_cast<float*>(out));
+  else if (action_dtype == IMENV_F32)
+    hipLaunchKernelGGL((imenv_cc_obs_kernel<double, float>), g, b, 0, st, static_cast<const double*>(obs),
+                       static_cast<const float*>(actions), n, num_agents, num_features, clip_lo, clip_hi,
+                       static_cast<double*>(out));
+  else
+    hipLaunchKernelGGL((imenv_cc_obs_kernel<double, double>), g, b, 0, st, static_cast<const double*>(obs),
+                       static_cast<const double*>(actions), n, num_agents, num_features, clip_lo, clip_hi,
+                       static_cast<double*>(out));
   HIPCHK(hipGetLastError());
   return IMENV_OK;
 }

@@ -20,7 +20,7 @@ def decode_config(cfg):
     return out
 
 
-NON_CASE = ("base_stock",)      # tools/gen_base_stock_fixtures.py, loaded by load_base_stock()
+NON_CASE = ("base_stock", "cc_obs")   # gen_base_stock_fixtures.py / gen_cc_fixtures.py (own loaders)
 
 
 def case_names():
