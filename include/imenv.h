@@ -286,6 +286,17 @@ int imenv_cc_observation(int64_t n, int32_t num_agents, int32_t num_features, co
                          const void* actions, int action_dtype, double clip_lo, double clip_hi, void* out,
                          void* stream);
 
+/* Generalised advantage estimation over a device rollout buffer: replaces the compute_advantages
+ * call of the trainers' postprocessing (models/CC_Policy.py:238-250; RLlib 1.5 compute_advantages
+ * with use_gae, discount_cumsum = scipy lfilter; gamma 0.99 / lambda 0.95 at utils.py:19-23).
+ * rewards / values: device [T][n] (float32 or float64), last_value: device [n] bootstrap value
+ * (value_dtype) or NULL for completed episodes (last_r = 0). Outputs float32 [T][n]: advantages and,
+ * if not NULL, value_targets = advantages + values. Arithmetic follows the reference's NumPy / SciPy
+ * dtypes and operation order (float64, or float32 deltas with a float32 bootstrap; imenv_gae_kernel). */
+int imenv_gae(int64_t n, int32_t T, const void* rewards, int reward_dtype, const void* values, int value_dtype,
+              const void* last_value, double gamma, double lambda, float* advantages, float* value_targets,
+              void* stream);
+
 /* State the reference's callers read directly (base_restock_policy.py:12:
  * env.inv/order_u/backlog[env.period]). Copies int32 [N][n] SoA into the given
  * device buffers (any may be NULL); *period (HOST) receives the current period. */

@@ -169,6 +169,48 @@ __global__ void __launch_bounds__(256) imenv_cc_obs_kernel(const OT* __restrict_
   }
 }
 
+// GAE over a [T][n] rollout (RLlib 1.5 compute_advantages with use_gae, as called by
+// models/CC_Policy.py:238-250; gamma / lambda from utils.py:19-23). One thread per env walks t from
+// T-1 down to 0; each step reads one coalesced row of rewards and values per wave. Arithmetic is
+// that of the reference path for a completed episode (last_r = 0.0 makes vpred_t float64):
+//   delta_t = (r_t + gamma * v_{t+1}) - v_t                     float64 (float32 terms with a float32
+//                                                               bootstrap value, see below)
+//   adv_t   = c * adv_{t+1} + delta_t, c = gamma * lambda      float64 (scipy lfilter's
+//             direct-form-II recursion of discount_cumsum; adv_{T-1} = 0.0 + delta_{T-1})
+//   advantages = float32(adv_t), value_targets = float32(adv_t + v_t)
+template <typename RT, typename VT>
+__global__ void __launch_bounds__(256) imenv_gae_kernel(const RT* __restrict__ rew, const VT* __restrict__ val,
+                                                        const VT* __restrict__ last, int64_t n, int T, double gamma,
+                                                        double c, float* __restrict__ adv_out,
+                                                        float* __restrict__ vt_out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  // a float32 bootstrap value keeps vpred_t float32 in the reference (np.concatenate of float32
+  // arrays), so gamma * v_{t+1} is a float32 product (NumPy casts the Python float to float32) and
+  // the sum / difference take the wider of the operands' types; last_r = 0.0 makes it all float64
+  const bool f32_path = sizeof(VT) == 4 && last != nullptr;
+  const float gamma32 = (float)gamma;
+  double vnext = last ? (double)last[e] : 0.0;
+  double adv = 0.0;
+  for (int t = T - 1; t >= 0; --t) {
+    const double v = (double)val[(int64_t)t * n + e];
+    const RT rr = rew[(int64_t)t * n + e];
+    const double r = (double)rr;
+    double delta;
+    if (f32_path) {
+      const float gv = gamma32 * (float)vnext;
+      if (sizeof(RT) == 4) delta = (double)(((float)rr + gv) - (float)v);
+      else delta = (r + (double)gv) - v;
+    } else {
+      delta = (r + gamma * vnext) - v;
+    }
+    adv = (t == T - 1) ? 0.0 + delta : c * adv + delta;
+    adv_out[(int64_t)t * n + e] = (float)adv;
+    if (vt_out) vt_out[(int64_t)t * n + e] = (float)(adv + v);
+    vnext = v;
+  }
+}
+
 thread_local std::string g_err;
 
 int fail(int code, const std::string& msg) {
@@ -808,6 +850,36 @@ int imenv_cc_observation(int64_t n, int32_t num_agents, int32_t num_features, co
     hipLaunchKernelGGL((imenv_cc_obs_kernel<double, double>), g, b, 0, st, static_cast<const double*>(obs),
                        static_cast<const double*>(actions), n, num_agents, num_features, clip_lo, clip_hi,
                        static_cast<double*>(out));
+  HIPCHK(hipGetLastError());
+  return IMENV_OK;
+}
+
+int imenv_gae(int64_t n, int32_t T, const void* rewards, int reward_dtype, const void* values, int value_dtype,
+              const void* last_value, double gamma, double lambda, float* advantages, float* value_targets,
+              void* stream) {
+  if (!rewards || !values || !advantages) return fail(IMENV_E_INVALID, "null argument");
+  if (n < 1 || T < 1) return fail(IMENV_E_INVALID, "n >= 1 and T >= 1");
+  if ((reward_dtype != IMENV_F32 && reward_dtype != IMENV_F64) || (value_dtype != IMENV_F32 && value_dtype != IMENV_F64))
+    return fail(IMENV_E_INVALID, "bad dtype");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const dim3 g((unsigned)((n + 255) / 256)), b(256);
+  const double c = gamma * lambda;
+  if (reward_dtype == IMENV_F32 && value_dtype == IMENV_F32)
+    hipLaunchKernelGGL((imenv_gae_kernel<float, float>), g, b, 0, st, static_cast<const float*>(rewards),
+                       static_cast<const float*>(values), static_cast<const float*>(last_value), n, T, gamma, c,
+                       advantages, value_targets);
+  else if (reward_dtype == IMENV_F64 && value_dtype == IMENV_F32)
+    hipLaunchKernelGGL((imenv_gae_kernel<double, float>), g, b, 0, st, static_cast<const double*>(rewards),
+                       static_cast<const float*>(values), static_cast<const float*>(last_value), n, T, gamma, c,
+                       advantages, value_targets);
+  else if (reward_dtype == IMENV_F32)
+    hipLaunchKernelGGL((imenv_gae_kernel<float, double>), g, b, 0, st, static_cast<const float*>(rewards),
+                       static_cast<const double*>(values), static_cast<const double*>(last_value), n, T, gamma, c,
+                       advantages, value_targets);
+  else
+    hipLaunchKernelGGL((imenv_gae_kernel<double, double>), g, b, 0, st, static_cast<const double*>(rewards),
+                       static_cast<const double*>(values), static_cast<const double*>(last_value), n, T, gamma, c,
+                       advantages, value_targets);
   HIPCHK(hipGetLastError());
   return IMENV_OK;
 }

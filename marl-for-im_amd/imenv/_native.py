@@ -83,6 +83,8 @@ SYMBOLS = [
     ("imenv_column_stats", c_int, [c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
     ("imenv_cc_observation", c_int, [c_int64, c_int32, c_int32, c_void_p, c_int, c_void_p, c_int, c_double, c_double,
                                      c_void_p, c_void_p]),
+    ("imenv_gae", c_int, [c_int64, c_int32, c_void_p, c_int, c_void_p, c_int, c_void_p, c_double, c_double, c_void_p,
+                          c_void_p, c_void_p]),
     ("imenv_get_state", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_int32), c_void_p]),
     ("imenv_get_errors", c_int, [c_void_p, c_void_p, POINTER(c_uint32), c_void_p]),
     ("imenv_dims", c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
