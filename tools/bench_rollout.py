@@ -115,6 +115,21 @@ def main():
         "mean_objective_policy0": float(out["stats"][0, 1, 0].item()),
         "cpu_baseline": cpu,
     }
+    # VALU-issue roofline from the committed PMC summary of this exact kernel variant
+    # (tools/profile_rollout.sh -> profiles/pmc_rollout_kernel.json): SQ_INSTS_VALU per launch over the
+    # rocprof-measured average duration of the rollout kernel alone
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_rollout_kernel.json")) as f:
+            pmc = json.load(f)
+        if pmc.get("kernel_info") and pmc["kernel_info"] in ro.kernel_info() and pmc.get("policies") == P \
+                and pmc.get("scenarios") == S:
+            ach = pmc["valu_wave_instr_per_launch"] / (pmc["kernel_avg_ns"] * 1e-9)
+            res["roofline"] = {"bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK, "unit": "wave-instr/s",
+                               "frac": round(ach / VALU_PEAK, 4),
+                               "valu_instr_per_env_step": round(pmc["valu_wave_instr_per_launch"] * 64 / steps, 1),
+                               "source": "profiles/pmc_rollout_kernel.json"}
+    except (OSError, ValueError, KeyError):
+        pass
     if cpu:
         res["gpu_over_cpu"] = round(res["value"] / cpu["value"], 1)
     print(json.dumps(res), flush=True)

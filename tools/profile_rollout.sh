@@ -1,6 +1,6 @@
 #!/bin/bash
-# Rollout kernel: bench line, kernel-trace stats and SQ counter passes (one counter group per pass,
-# --pmc only). Run on the GPU box from the repo root.
+# Rollout kernel: bench lines, kernel-trace stats and SQ counter passes (one counter group per pass,
+# --pmc only), summarised into $OUT/pmc_rollout_kernel.json. Run on the GPU box from the repo root.
 OUT=${1:-gpurun_out/rollout}
 export TMPDIR=/tmp
 mkdir -p $OUT
@@ -8,10 +8,10 @@ B="python tools/bench_rollout.py --no-cpu --reps 5"
 timeout -k 10 300 python tools/bench_rollout.py > $OUT/bench.json 2> $OUT/bench.err &&
 timeout -k 10 300 python tools/bench_rollout.py --config IM8 --no-cpu > $OUT/bench_im8.json 2>> $OUT/bench.err &&
 timeout -k 10 300 python tools/bench_rollout.py --config IM_div1 --no-cpu > $OUT/bench_div1.json 2>> $OUT/bench.err &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/trace -o p --output-format csv -- $B > $OUT/trace.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/trace -o p --output-format csv -- $B > $OUT/bench_prof.json 2> $OUT/trace.log &&
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $GRAFT_REPO_ROOT/$OUT/sq1 -o p --output-format csv -- $B > $OUT/sq1.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS -d $GRAFT_REPO_ROOT/$OUT/sq2 -o p --output-format csv -- $B > $OUT/sq2.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS -d $GRAFT_REPO_ROOT/$OUT/sq2 -o p --output-format csv -- $B > $OUT/sq2.log 2>&1 &&
+python tools/rollout_pmc_summary.py $OUT > $OUT/pmc_rollout_kernel.json
 rc=$?
-python tools/pmc_summary.py $OUT/summary.json 0 $OUT/sq1 $OUT/sq2 > $OUT/summary.log 2>&1
 echo "profile_rollout rc=$rc"
 exit $rc
