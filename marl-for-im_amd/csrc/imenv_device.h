@@ -350,7 +350,8 @@ struct DynSpec {
   static constexpr bool EXACT = NT_ <= 8;    // AOT kernels for N <= 8 are compiled for N == NT
   static constexpr bool JIT = false;
   static constexpr int TAB_LDS = IMENV_TABLE_MAX;   // Poisson table staged in LDS
-  static constexpr int BS = 256;                     // threads (= envs) per block
+  static constexpr int BS = 256;                     // threads per block
+  static constexpr int EPT = 1;                      // envs per thread
   using ST = ST_;
   const SpecDev* __restrict__ sp;
   const StepArgs& A;
@@ -645,45 +646,50 @@ __device__ __forceinline__ void step_core(const P& p, const int t, const int (&o
 // Structure: (A) issue every load that does not depend on this step's arithmetic (raw words),
 // (B) compute in registers, (C) store; float32 BASE observations are staged through LDS so the
 // block writes its contiguous obs slab with full 1 KiB-per-wave float4 stores.
+// Per-env raw words of one step, loaded before any of them is used (step_load) so that the loads
+// of all the envs a thread owns overlap; step_finish unpacks and computes.
 template <class P>
-__device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_t* s_tab, float* s_obs) {
+struct StepLoad {
+  using R = Row<typename P::ST, P::NT, P::EXACT>;
+  using R32 = Row<int32_t, P::NT, P::EXACT>;
+  uint32_t aw[2 * P::NT];
+  uint32_t w_inv[R::WORDS], w_bl[R::WORDS], w_ou[R::WORDS], w_cin[R32::WORDS], w_bto[R32::WORDS];
+  typename P::ST r_arr[P::NT];
+  int cdem[P::NT];
+  double du[P::NT];
+  double macc[4 + P::NT];
+};
+
+template <class P>
+__device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const int64_t e, StepLoad<P>& L) {
   constexpr int NT = P::NT;
   constexpr int MC = P::MC;
   constexpr bool EXACT = P::EXACT;
-  constexpr bool STAGE = P::BASE && NT <= 8;
   using ST = typename P::ST;
   using R = Row<ST, NT, EXACT>;
   using R32 = Row<int32_t, NT, EXACT>;
-  const int tid = threadIdx.x;
-  constexpr int BS = P::BS;
-  const int64_t e0 = (int64_t)blockIdx.x * BS;
-  const int64_t e = e0 + tid;
   const int64_t n = A.n;
   const bool valid = e < n;
   const int N = p.N();
   const int np = p.np();
   const int t = A.t;
-  const bool poisson = p.demand_layout() == IMENV_LAYOUT_DRAW && p.demand_dist() == IMENV_DEMAND_POISSON;
-  const uint32_t ep = *A.episode;   // scalar load issued first: the draws below need it
-  const uint32_t gid = A.env_offset + (uint32_t)e;
-  const uint64_t seed = p.seed();
-  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-
-  ST* __restrict__ p_inv = static_cast<ST*>(A.inv);
-  ST* __restrict__ p_bl = static_cast<ST*>(A.bl);
-  ST* __restrict__ p_ou = static_cast<ST*>(A.ou);
-  ST* __restrict__ p_ring = static_cast<ST*>(A.ring);
-  int32_t* __restrict__ p_carry = A.carry;
-  int32_t* __restrict__ p_bto = A.bto;
-  const int64_t ring_rows = n * np;   // elements per packed-row array (history)
-
+  const ST* __restrict__ p_inv = static_cast<const ST*>(A.inv);
+  const ST* __restrict__ p_bl = static_cast<const ST*>(A.bl);
+  const ST* __restrict__ p_ou = static_cast<const ST*>(A.ou);
+  const ST* __restrict__ p_ring = static_cast<const ST*>(A.ring);
+  const int32_t* __restrict__ p_carry = A.carry;
+  const int32_t* __restrict__ p_bto = A.bto;
   // ================= (A) loads: raw words only, every independent load issued before any use
-  uint32_t aw[2 * NT];
-  uint32_t w_inv[R::WORDS], w_bl[R::WORDS], w_ou[R::WORDS], w_cin[R32::WORDS], w_bto[R32::WORDS];
-  ST r_arr[NT];
-  int cdem[NT];
-  double du[NT];
-  double macc[4 + NT];
+  uint32_t (&aw)[2 * NT] = L.aw;
+  uint32_t (&w_inv)[R::WORDS] = L.w_inv;
+  uint32_t (&w_bl)[R::WORDS] = L.w_bl;
+  uint32_t (&w_ou)[R::WORDS] = L.w_ou;
+  uint32_t (&w_cin)[R32::WORDS] = L.w_cin;
+  uint32_t (&w_bto)[R32::WORDS] = L.w_bto;
+  ST (&r_arr)[NT] = L.r_arr;
+  int (&cdem)[NT] = L.cdem;
+  double (&du)[NT] = L.du;
+  double (&macc)[4 + NT] = L.macc;
 #pragma unroll
   for (int k = 0; k < 4 + NT; ++k) macc[k] = 0.0;
 #pragma unroll
@@ -743,7 +749,50 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
       for (int k = 0; k < 4 + NT; ++k) if (k < 4 + N) macc[k] = A.metrics[el * (4 + N) + k];
     }
   }
-  p.stage_tables(s_tab, poisson);
+}
+
+// One env's step after its loads: the random draws, unpack, step_core, the stores and the next
+// observation. With a staged float32 base observation the row goes to the block's LDS slab s_obs
+// (written out by step_body after a barrier); every other observation is stored directly.
+template <class P>
+__device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const int64_t e, const StepLoad<P>& L,
+                                            uint32_t* s_tab, float* s_obs) {
+  constexpr int NT = P::NT;
+  constexpr int MC = P::MC;
+  constexpr bool EXACT = P::EXACT;
+  constexpr bool STAGE = P::BASE && NT <= 8;
+  using ST = typename P::ST;
+  using R = Row<ST, NT, EXACT>;
+  using R32 = Row<int32_t, NT, EXACT>;
+  const int tid = threadIdx.x;
+  const int64_t n = A.n;
+  const bool valid = e < n;
+  const int N = p.N();
+  const int np = p.np();
+  const int t = A.t;
+  const bool poisson = p.demand_layout() == IMENV_LAYOUT_DRAW && p.demand_dist() == IMENV_DEMAND_POISSON;
+  const uint32_t ep = *A.episode;
+  const uint32_t gid = A.env_offset + (uint32_t)e;
+  const uint64_t seed = p.seed();
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+
+  ST* __restrict__ p_inv = static_cast<ST*>(A.inv);
+  ST* __restrict__ p_bl = static_cast<ST*>(A.bl);
+  ST* __restrict__ p_ou = static_cast<ST*>(A.ou);
+  ST* __restrict__ p_ring = static_cast<ST*>(A.ring);
+  int32_t* __restrict__ p_carry = A.carry;
+  int32_t* __restrict__ p_bto = A.bto;
+  const int64_t ring_rows = n * np;   // elements per packed-row array (history)
+  const uint32_t (&aw)[2 * NT] = L.aw;
+  const uint32_t (&w_inv)[R::WORDS] = L.w_inv;
+  const uint32_t (&w_bl)[R::WORDS] = L.w_bl;
+  const uint32_t (&w_ou)[R::WORDS] = L.w_ou;
+  const uint32_t (&w_cin)[R32::WORDS] = L.w_cin;
+  const uint32_t (&w_bto)[R32::WORDS] = L.w_bto;
+  const ST (&r_arr)[NT] = L.r_arr;
+  const int (&cdem)[NT] = L.cdem;
+  const double (&du)[NT] = L.du;
+  const double (&macc)[4 + NT] = L.macc;
 
   // (A2) random draws depend on no loaded value: placed before the first use of a load, they
   // execute under the loads' latency instead of after the wait
@@ -923,17 +972,6 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           }
         }
       }
-      __syncthreads();
-      const int64_t cnt = (n - e0) < BS ? (n - e0) : BS;
-      const int64_t total = cnt * row;
-      float* gobs = static_cast<float*>(A.obs) + e0 * row;
-      if ((total & 3) == 0) {
-        float4* g4 = reinterpret_cast<float4*>(gobs);
-        const float4* s4 = reinterpret_cast<const float4*>(s_obs);
-        for (int64_t q = tid; q < total / 4; q += BS) g4[q] = s4[q];
-      } else {
-        for (int64_t q = tid; q < total; q += BS) gobs[q] = s_obs[q];
-      }
     } else if (valid) {
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
@@ -1012,6 +1050,51 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
     } else {
 #pragma unroll 1
       for (int f = 0; f < F; ++f) feature(f);
+    }
+  }
+}
+
+// The step kernel body: each thread owns P::EPT envs, one per BS-env slab of the block's EPT*BS
+// envs (env = (blockIdx * EPT + k) * BS + tid). Every load of every owned env is issued first, then
+// each env is finished in turn; a staged float32 base observation is written out slab by slab as
+// contiguous float4 runs after one barrier.
+template <class P>
+__device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_t* s_tab, float* s_obs) {
+  constexpr int NT = P::NT;
+  constexpr int BS = P::BS;
+  constexpr int EPT = P::EPT;
+  constexpr bool STAGE = P::BASE && NT <= 8;
+  const int tid = threadIdx.x;
+  const int64_t n = A.n;
+  const int64_t eb = (int64_t)blockIdx.x * EPT * BS;
+  const bool poisson = p.demand_layout() == IMENV_LAYOUT_DRAW && p.demand_dist() == IMENV_DEMAND_POISSON;
+  StepLoad<P> L[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) step_load(p, A, eb + k * BS + tid, L[k]);
+  p.stage_tables(s_tab, poisson);
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) step_finish(p, A, eb + k * BS + tid, L[k], s_tab, s_obs + k * (BS * 3 * NT));
+  if constexpr (P::BASE && STAGE) {
+    if (!p.obs_f64()) {
+      __syncthreads();
+      const int row = 3 * p.N();
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) {
+        const int64_t e0 = eb + k * BS;
+        if (e0 < n) {
+          const int64_t cnt = (n - e0) < BS ? (n - e0) : BS;
+          const int64_t total = cnt * row;
+          float* gobs = static_cast<float*>(A.obs) + e0 * row;
+          const float* so = s_obs + k * (BS * 3 * NT);
+          if ((total & 3) == 0) {
+            float4* g4 = reinterpret_cast<float4*>(gobs);
+            const float4* s4 = reinterpret_cast<const float4*>(so);
+            for (int64_t q = tid; q < total / 4; q += BS) g4[q] = s4[q];
+          } else {
+            for (int64_t q = tid; q < total; q += BS) gobs[q] = so[q];
+          }
+        }
+      }
     }
   }
 }
@@ -1275,7 +1358,7 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
 // obs staging buffer size (floats) for a policy
 template <class P>
 constexpr int stage_floats() {
-  return (P::BASE && P::NT <= 8) ? P::BS * 3 * P::NT : 4;
+  return (P::BASE && P::NT <= 8) ? P::EPT * P::BS * 3 * P::NT : 4;
 }
 
 // Kernel template for any policy whose constructor takes (spec, args).

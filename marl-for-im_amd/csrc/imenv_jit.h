@@ -38,7 +38,8 @@ struct JitFlags {
 struct JitKernel {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr;
-  int bs = 256;       // threads (= envs) per block
+  int bs = 256;       // threads per block
+  int ept = 1;        // envs per thread (step kernel)
   std::string tag;    // short description (kernel_info)
 };
 

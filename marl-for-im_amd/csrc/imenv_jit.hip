@@ -67,6 +67,17 @@ int jit_block_size() {
   return bs;
 }
 
+// Envs per thread of the JIT step kernel (step_body). 1: with two envs per thread the footprint probe
+// gets 5% faster (tools/probe3.py: 19.35 vs 20.42 us at C2 size), but the real kernel gets slower
+// (23.4 vs 21.0 us: twice the registers, a 24 KiB obs slab per block), profiles/r01/probe3_u8_floor.log.
+// IMENV_JIT_EPT=2 selects it (only for the staged base-observation layout, N <= 8).
+int jit_envs_per_thread(const SpecDev& d, bool base) {
+  int ept = 1;
+  if (const char* v = std::getenv("IMENV_JIT_EPT")) ept = std::atoi(v) == 2 ? 2 : 1;
+  if (!(base && d.s.num_nodes <= 8)) ept = 1;
+  return ept;
+}
+
 // The reference's observation value a + (v * (b - a)) / den (IM_env.py:435-444), in the same IEEE
 // double expression as the device's obs_map (both built with -ffp-contract=off).
 double ref_obs(const ImEnvSpec& s, int g, int i, int v) {
@@ -136,7 +147,7 @@ void emit_obs_hooks(std::ostream& o, const SpecDev& d) {
 
 namespace {
 // The JitSpec policy class: every accessor step_body / rollout_body use, as a constexpr.
-void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const JitFlags& f, int bs) {
+void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const JitFlags& f, int bs, int ept) {
   const ImEnvSpec& s = d.s;
   const int N = s.num_nodes;
   const int F = s.num_features;
@@ -154,6 +165,7 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
     << "  static constexpr bool JIT = true;\n"
     << "  static constexpr int TAB_LDS = " << (inline_tab ? 1 : IMENV_TABLE_MAX) << ";\n"
     << "  static constexpr int BS = " << bs << ";\n"
+    << "  static constexpr int EPT = " << ept << ";\n"
     << "  static constexpr int RING = " << d.ring_total << ";\n"
     << "  using ST = " << (d.es == 1 ? "uint8_t" : d.es == 2 ? "int16_t" : "int32_t") << ";\n"
     << "  const imenv::SpecDev* __restrict__ sp;\n"
@@ -243,7 +255,7 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
 
 std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f) {
   std::ostringstream o;
-  emit_policy(o, d, maxc, base, f, jit_block_size());
+  emit_policy(o, d, maxc, base, f, jit_block_size(), jit_envs_per_thread(d, base));
   o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
        "imenv_step_jit(const imenv::SpecDev* __restrict__ sp, const imenv::StepArgs A) {\n"
        "  __shared__ uint32_t s_tab[JitSpec::TAB_LDS];\n"
@@ -350,9 +362,10 @@ bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const st
   const std::string src = jit_source(d, maxc, base, f);
   if (!load_module(src, arch, "imenv_step_jit", out, msg)) return false;
   out.bs = jit_block_size();
+  out.ept = jit_envs_per_thread(d, base);
   char tag[160];
-  std::snprintf(tag, sizeof tag, "jit:imenv_step_jit[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,%zuB]",
-                d.s.num_nodes, maxc, base ? 1 : 0, d.es, f.key(), out.bs, src.size());
+  std::snprintf(tag, sizeof tag, "jit:imenv_step_jit[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,ept=%d,%zuB]",
+                d.s.num_nodes, maxc, base ? 1 : 0, d.es, f.key(), out.bs, out.ept, src.size());
   out.tag = tag;
   return true;
 }
@@ -361,7 +374,8 @@ hipError_t jit_launch(const JitKernel& k, hipStream_t st, const SpecDev* sp, con
   const SpecDev* spv = sp;
   StepArgs av = A;
   void* args[] = {&spv, &av};
-  const unsigned grid = (unsigned)((A.n + k.bs - 1) / k.bs);
+  const int64_t per_block = (int64_t)k.bs * k.ept;
+  const unsigned grid = (unsigned)((A.n + per_block - 1) / per_block);
   return hipModuleLaunchKernel(k.fn, grid, 1, 1, (unsigned)k.bs, 1, 1, 0, st, args, nullptr);
 }
 
@@ -381,7 +395,7 @@ std::string jit_rollout_source(const SpecDev& d, int maxc, const RolloutFlags& f
   jf.noisy_demand = f.noisy_demand;
   jf.demand_layout = f.table ? IMENV_LAYOUT_PER_ENV : IMENV_LAYOUT_DRAW;
   std::ostringstream o;
-  emit_policy(o, d, maxc, false, jf, bs);
+  emit_policy(o, d, maxc, false, jf, bs, 1);
   const int pmf = f.objective ? kRolloutPmfLds : 1;
   o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
        "imenv_rollout_jit(const imenv::SpecDev* __restrict__ sp, const imenv::RolloutArgs A) {\n"
