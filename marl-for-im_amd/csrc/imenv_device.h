@@ -179,18 +179,25 @@ __device__ __forceinline__ uint32_t rng_word(uint32_t gid, uint32_t ep, int t, u
   return word_of(rng_block(gid, ep, t, stream, lane, k0, k1), t & 3);
 }
 
-__device__ __forceinline__ int ceil_div_pos(int a, int b) { return (a + b - 1) / b; }
+// ceil(a / b) for a > 0, 1 <= b <= 8 (b = number of eligible children): the common b = 1, 2 without
+// an integer division
+__device__ __forceinline__ int ceil_div_pos(int a, int b) {
+  if (b == 1) return a;
+  if (b == 2) return (a + 1) >> 1;
+  return (a + b - 1) / b;
+}
 
 // Round-robin unit shipping, closed form. Restates the reference's
 //   while <cond> and amt > 0: for k in children: if x[k] > 0: s[k]+=1; x[k]-=1; amt-=1
 // (IM_div_env.py:413-428, 440-450, 472-484; the inner loop does not re-check amt).
-// SUMCHECK: loop also requires sum(x) > 0 (backlog-first / outstanding-order loops).
-// Without it (capped loop, IM_div_env.py:488-498) an env with nothing eligible spins
-// until the guard trips. Phases: while the set P = {k: x[k] > 0} is fixed, every
-// round moves |P| units, so a phase lasts min(min_P x, ceil(S/|P|), ceil(amt/|P|))
-// rounds. Returns false if the guard (rounds > lim) trips; rounds stop at lim+1.
-template <int MC, bool SUMCHECK>
-__device__ __forceinline__ bool rr_closed(int m, int (&x)[MC], int (&s)[MC], int& amt, int lim) {
+// sumcheck: the loop also requires sum(x) > 0 (backlog-first / outstanding-order loops). Without it
+// (capped loop, IM_div_env.py:488-498) an env with nothing eligible spins until the guard trips.
+// Phases: while the set P = {k: x[k] > 0} is fixed, every round moves |P| units, so a phase lasts
+// min(min_P x, ceil(S/|P|), ceil(amt/|P|)) rounds. Returns false if the guard (rounds > lim) trips;
+// rounds stop at lim+1. amt <= 0 returns true at once. sumcheck is a per-lane value so that every
+// branch of the split runs this one loop (no divergent copies of it in a wave).
+template <int MC>
+__device__ __forceinline__ bool rr_closed(int m, int (&x)[MC], int (&s)[MC], int& amt, int lim, bool sumcheck) {
   int rounds = 0;
 #pragma unroll 1
   for (int ph = 0; ph <= MC + 1; ++ph) {
@@ -203,10 +210,10 @@ __device__ __forceinline__ bool rr_closed(int m, int (&x)[MC], int (&s)[MC], int
       }
     }
     if (amt <= 0) break;
-    if (SUMCHECK && S <= 0) break;
+    if (sumcheck && S <= 0) break;
     if (cnt == 0) { rounds = lim + 1; break; }   // no progress possible: guard trips
     int r = min(mn, ceil_div_pos(amt, cnt));
-    if (SUMCHECK) r = min(r, ceil_div_pos(S, cnt));
+    if (sumcheck) r = min(r, ceil_div_pos(S, cnt));
     const int rem = lim + 1 - rounds;
     if (r > rem) r = rem;
 #pragma unroll
@@ -554,34 +561,36 @@ __device__ __forceinline__ void step_core(const P& p, const int t, const int (&o
           bto[k] = sel<NT>(btoc, c);
         }
       }
-      int amt = shp;
-      bool ok = true;
-      if (shp >= dmp) {
-        if (blp > 0) {        // backlog first, then outstanding orders (IM_div_env.py:409-454)
-          ok = rr_closed<MC, true>(m, bto, s, amt, p.split_limit(q, 0));
-          if (ok && amt > 0 && dmp > 0) {
-            int out[MC];
+      // the four branches of IM_div_env.py:409-502 as one straight-line sequence (per-lane choices,
+      // one round-robin loop that every lane runs):
+      //   A ship >= demand, backlog > 0: backlog-first loop over backlog_to, then outstanding orders
+      //   B ship >= demand, no backlog:  ship_to += order                      (IM_div_env.py:457-460)
+      //   C ship <  demand, backlog > 0: backlog-first loop, backlog_to += order - ship_to (:468-484, 501)
+      //   D ship <  demand, no backlog:  loop capped at order + backlog_to, then the same (:486-502)
+      const bool caseA = shp >= dmp && blp > 0;
+      const bool caseB = shp >= dmp && blp <= 0;
+      const bool caseD = shp < dmp && blp <= 0;
+      int x1[MC];
 #pragma unroll
-            for (int k = 0; k < MC; ++k) out[k] = oc[k];
-            ok = rr_closed<MC, true>(m, out, s, amt, p.split_limit(q, 1));
+      for (int k = 0; k < MC; ++k) x1[k] = caseD ? oc[k] + bto[k] : bto[k];
+      int amt = caseB ? 0 : shp;
+      const int lim1 = caseA ? p.split_limit(q, 0) : (caseD ? p.split_limit(q, 3) : p.split_limit(q, 2));
+      bool ok = rr_closed<MC>(m, x1, s, amt, lim1, !caseD);
+      if (!caseD) {
 #pragma unroll
-            for (int k = 0; k < MC; ++k) bto[k] += out[k];
-          }
-        } else {              // IM_div_env.py:457-460
+        for (int k = 0; k < MC; ++k) bto[k] = x1[k];   // A and C drain backlog_to in place
+      }
+      const bool second = caseA && ok && amt > 0 && dmp > 0;
+      int out[MC];
 #pragma unroll
-          for (int k = 0; k < MC; ++k) s[k] += oc[k];
-        }
-      } else {
-        if (blp > 0) {        // IM_div_env.py:468-484
-          ok = rr_closed<MC, true>(m, bto, s, amt, p.split_limit(q, 2));
-        } else {              // IM_div_env.py:486-498: cap at order + backlog_to
-          int cap[MC];
+      for (int k = 0; k < MC; ++k) out[k] = oc[k];
+      int amt2 = second ? amt : 0;
+      ok = rr_closed<MC>(m, out, s, amt2, p.split_limit(q, 1), true) && ok;
 #pragma unroll
-          for (int k = 0; k < MC; ++k) cap[k] = oc[k] + bto[k];
-          ok = rr_closed<MC, false>(m, cap, s, amt, p.split_limit(q, 3));
-        }
-#pragma unroll
-        for (int k = 0; k < MC; ++k) bto[k] += oc[k] - s[k];   // IM_div_env.py:501-502
+      for (int k = 0; k < MC; ++k) {
+        if (second) bto[k] += out[k];
+        if (caseB) s[k] += oc[k];
+        if (!caseA && !caseB) bto[k] += oc[k] - s[k];   // IM_div_env.py:501-502
       }
       split_ok = split_ok && ok;
 #pragma unroll

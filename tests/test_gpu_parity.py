@@ -254,3 +254,17 @@ def test_gpu_narrowest_layout_selected():
     env = VectorInvEnv(meta["kind"], meta["config"], n_envs=4, device=DEV)
     assert env.state_layout()[0] == 2
     env.close()
+
+
+@pytest.mark.parametrize("name", ["C2_MAIM4", "C3_IM8", "IM_div1"])
+def test_gpu_two_envs_per_thread_variant(name, kernel_mode, monkeypatch):
+    """The JIT kernel's two-envs-per-thread layout (IMENV_JIT_EPT=2, staged float32 observations)
+    computes the same function; 32 golden envs do not fill one 512-env block (ragged slabs)."""
+    if kernel_mode != "jit":
+        pytest.skip("JIT-only variant")
+    monkeypatch.setenv("IMENV_JIT_EPT", "2")
+    meta, d = load_case(name)
+    obs0, out, _ = run_gpu_case(meta, d, obs_dtype=torch.float32)
+    np.testing.assert_array_equal(out["obs"], d["obs"].astype(np.float32))
+    for k in ("inv", "backlog", "order_u"):
+        np.testing.assert_array_equal(out[k].astype(np.float64), d[k])
