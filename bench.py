@@ -134,6 +134,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--gather", action="store_true", help="add the per-step RCCL all-gather of obs+reward")
     ap.add_argument("--cpu-only", action="store_true", help=argparse.SUPPRESS)
+    # rehearsal of the multi-rank path on a one-GPU box: every rank on device 0, gloo for the
+    # barrier / max-reduction (the driver's N-GPU runs use one GPU per rank and RCCL)
+    ap.add_argument("--rehearse-one-gpu", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_only:
         print(json.dumps(_cpu_baseline_here(args.cpu_seconds)))
@@ -153,10 +156,15 @@ def main():
     from imenv import _native as nat
     from imenv.shard import StepGather, weak_offset
 
+    if args.rehearse_one_gpu:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     n = args.n_envs
     env = VectorInvEnv("MAIM", C2_CONFIG, n_envs=n, device=dev, env_offset=weak_offset(n, rank))
@@ -262,8 +270,9 @@ def main():
         "data": "synthetic: in-kernel Philox4x32-10 Poisson(5) demand, uniform[-1,1] f32 actions (torch seed 0)",
         "config": {
             "workload": "C2 shape at the metric's size: MultiAgentInvManagement 4-stage serial "
-                        "(inv_management.py:35-56 constants, MA_1 flags, shared reward), 2^20 envs per GPU, "
-                        "30-period episodes with the reset inside the timed loop",
+                        "(inv_management.py:35-56 constants, MA_1 flags, shared reward), %s envs per GPU, "
+                        "30-period episodes with the reset inside the timed loop"
+                        % ("2^20" if n == 1 << 20 else str(n)),
             "n_envs_per_gpu": n, "global_envs": world * n, "num_stages": N, "obs_features": F,
             "num_periods": T, "parallelism": "env-sharded x%d (one process per GPU, no data-path collective%s)"
                                              % (world, ", + RCCL all-gather of obs/reward per step" if gather is not None else ""),
