@@ -44,34 +44,41 @@ C2_CONFIG = dict(num_stages=4, num_periods=30, init_inv=np.ones(4) * 10, inv_tar
                  prev_demand=False, prev_actions=False, prev_length=1, independent=False)
 
 
-def step_bytes(spec, es):
-    """Algorithmic HBM bytes per env-step of the step kernel, averaged over an episode.
-
-    es = state element bytes (2: int16 packed state, 4: int32). Steady state:
-    actions 4N (f32) + state 3 fields x N x es read + write + arrivals N x es read +
-    departures N x es write + obs 4NF (f32) + reward 8 (f64 shared; 8N independent).
-    Per-episode average of the MINIMAL bytes: period 0 needs no state read (the initial
-    state is implicit) and node i needs no arrival read while t < delay_i.
-    """
-    N, F, T = spec.num_nodes, spec.num_features, spec.num_periods
-    rew = 8 * N if spec.reward_mode == 2 else 8
-    steady = 4 * N + 6 * N * es + 2 * N * es + 4 * N * F + rew
-    skipped = 3 * N * es + es * int(np.minimum(spec.delay, T).sum())   # per episode
-    return steady, steady - skipped / T
+C3_CONFIG = dict(num_stages=8, num_periods=30, init_inv=np.ones(8) * 10, inv_target=np.zeros(8),
+                 inv_max=np.ones(8) * 30, price=np.array([9, 8, 7, 6, 5, 4, 3, 2, 1]),
+                 stock_cost=np.array([0.35, 0.3, 0.4, 0.2, 0.35, 0.3, 0.4, 0.2]),
+                 backlog_cost=np.array([0.5, 0.7, 0.6, 0.9, 0.5, 0.7, 0.6, 0.9]),
+                 delay=np.array([1, 2, 3, 1, 4, 2, 3, 1]), demand_dist="poisson", mu=5, seed=52)
+C4_CONFIG = dict(num_nodes=4, connections={0: [1], 1: [2, 3], 2: [], 3: []}, num_periods=30,
+                 init_inv=np.ones(4) * 10, inv_target=np.zeros(4), inv_max=np.ones(4) * 30,
+                 stock_cost=np.array([0.35, 0.3, 0.4, 0.4]), backlog_cost=np.array([0.5, 0.7, 0.6, 0.6]),
+                 delay=np.array([1, 2, 1, 1]), demand_dist="poisson", mu=5, seed=52, time_dependency=True,
+                 prev_demand=True, prev_actions=False, prev_length=1, independent=False)
+# name -> (env kind, config, description, BASELINE.json size). C2 at 2^20 envs is the metric's workload
+# (the default); C3 / C4 are BASELINE's other single-GPU configs (parity cases; --config selects them)
+CONFIGS = {
+    "C2": ("MAIM", C2_CONFIG, "MultiAgentInvManagement 4-stage serial (inv_management.py:35-56 constants, "
+                              "MA_1 flags, shared reward)", 1 << 20),
+    "C3": ("IM", C3_CONFIG, "InvManagement 8-stage serial chain (SHLP_8.py:26-46 constants, flags off)", 262144),
+    "C4": ("MAIM_div", C4_CONFIG, "MultiAgentInvManagementDiv div1 2-retailer tree (MA_inv_management_div.py:46-69, "
+                                  "MA_6 flags: time_dependency + prev_demand L=1, shared reward)", 131072),
+}
 
 
 # ----------------------------------------------------------------- CPU baseline
 def _cpu_worker(args):
-    seconds, seed = args
+    seconds, seed, cname = args
     os.environ["OMP_NUM_THREADS"] = "1"
     from oracle.im_oracle import OracleEnv
+    kind, cfg = CONFIGS[cname][:2]
     rs = np.random.RandomState(seed)
-    env = OracleEnv("MAIM", C2_CONFIG, n_envs=1)
+    env = OracleEnv(kind, cfg, n_envs=1)
+    N, R = env.N, len(env.retailers)
     steps = 0
     t0 = time.perf_counter()
     while True:
-        dem = rs.poisson(5, 30)
-        act = rs.uniform(-1, 1, size=(30, 1, 4)).astype(np.float32).astype(np.float64)
+        dem = rs.poisson(5, 30) if kind in ("IM", "MAIM") else rs.poisson(5, (1, R, 30))
+        act = rs.uniform(-1, 1, size=(30, 1, N)).astype(np.float32).astype(np.float64)
         env.reset(customer_demand=dem)
         for t in range(30):
             env.step(act[t])
@@ -81,30 +88,31 @@ def _cpu_worker(args):
             return steps, el
 
 
-def cpu_baseline(seconds=1.5):
+def cpu_baseline(seconds=1.5, cname="C2"):
     """Oracle port of the reference step(), one env per process (the reference's own usage:
     one env per RLlib worker), a pool over this box's cores. Runs in a child interpreter
     started with BLAS threads pinned to 1 (they must be set before numpy is imported)."""
     import subprocess
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
-    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-only", "--cpu-seconds", str(seconds)],
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-only", "--cpu-seconds", str(seconds),
+                        "--config", cname],
                        env=env, capture_output=True, text=True, timeout=600)
     if r.returncode != 0:
         raise RuntimeError("cpu baseline failed: " + r.stderr[-2000:])
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-def _cpu_baseline_here(seconds):
+def _cpu_baseline_here(seconds, cname):
     cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
     ctx = mp.get_context("fork")   # before any GPU call in this process: plain fork, no exec
     with ctx.Pool(cores) as pool:
-        res = pool.map(_cpu_worker, [(seconds, 100 + i) for i in range(cores)])
+        res = pool.map(_cpu_worker, [(seconds, 100 + i, cname) for i in range(cores)])
     total = sum(s / e for s, e in res)
     return dict(value=round(total, 1), unit="env-steps/s", cores=cores, kind="port",
-                sample="oracle/im_oracle.py MAIM 4-stage (C2 constants), 1 env per process, %d processes x "
+                sample="oracle/im_oracle.py %s (%s config), 1 env per process, %d processes x "
                        "%.1f s of whole 30-period episodes each (%d env-steps total), host-fed Poisson(5) demand, "
-                       "BLAS threads 1; per core %.0f env-steps/s" % (cores, seconds, sum(s for s, _ in res),
-                                                                     total / cores))
+                       "BLAS threads 1; per core %.0f env-steps/s" % (CONFIGS[cname][0], cname, cores, seconds,
+                                                                     sum(s for s, _ in res), total / cores))
 
 
 # ----------------------------------------------------------------- PMC traffic
@@ -129,7 +137,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=60)
-    ap.add_argument("--n-envs", type=int, default=1 << 20, help="envs per GPU")
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS),
+                    help="C2 (default): the metric's workload; C3 / C4: BASELINE's other single-GPU configs")
+    ap.add_argument("--n-envs", type=int, default=None,
+                    help="envs per GPU (default: 2^20 for C2, BASELINE.json's size for C3 / C4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--gather", action="store_true", help="add the per-step RCCL all-gather of obs+reward")
@@ -139,7 +150,7 @@ def main():
     ap.add_argument("--rehearse-one-gpu", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_only:
-        print(json.dumps(_cpu_baseline_here(args.cpu_seconds)))
+        print(json.dumps(_cpu_baseline_here(args.cpu_seconds, args.config)))
         return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -148,7 +159,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds)          # before the GPU is initialised
+        cpu = cpu_baseline(args.cpu_seconds, args.config)          # before the GPU is initialised
 
     import torch
     import torch.distributed as dist
@@ -166,15 +177,16 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
 
-    n = args.n_envs
-    env = VectorInvEnv("MAIM", C2_CONFIG, n_envs=n, device=dev, env_offset=weak_offset(n, rank))
+    kind, ccfg, cdesc, cn = CONFIGS[args.config]
+    n = args.n_envs or cn
+    env = VectorInvEnv(kind, ccfg, n_envs=n, device=dev, env_offset=weak_offset(n, rank))
     N, F, T = env.N, env.F, env.T
     g = torch.Generator(device=dev)
     g.manual_seed(0)
     actions = torch.rand((T, n, N), generator=g, device=dev, dtype=torch.float32) * 2 - 1
     obs_buf = torch.empty((T, n, N, F), dtype=torch.float32, device=dev)
     obs0 = torch.empty((n, N, F), dtype=torch.float32, device=dev)
-    rew_buf = torch.empty((T, n), dtype=torch.float64, device=dev)
+    rew_buf = torch.empty((T,) + env.reward_shape(), dtype=torch.float64, device=dev)
     gather = None
     if args.gather and world > 1:
         gather = StepGather(obs_buf[0], rew_buf[0])
@@ -235,7 +247,8 @@ def main():
 
     # measured stream-copy ceiling at the step's byte count: a device copy of half the
     # bytes moves them once in and once out; outside the timed region
-    half = max(1 << 20, int(step_bytes(env.spec, env.state_layout()[0])[1] * n) // 2 // 16 * 16)
+    b_steady, b_avg = env.step_traffic()
+    half = max(1 << 20, int(b_avg * n) // 2 // 16 * 16)
     csrc = torch.empty(half // 4, dtype=torch.float32, device=dev)
     cdst = torch.empty_like(csrc)
     for _ in range(3):
@@ -252,7 +265,6 @@ def main():
     total_env_steps = world * n * K
     value = total_env_steps / el
     es = env.state_layout()[0]
-    b_steady, b_avg = step_bytes(env.spec, es)
     achieved_gbs = (b_avg * n) / (kern_ms * 1e-3) / 1e9
     traffic = pmc_traffic(n, env.kernel_info())
     out = {
@@ -269,10 +281,9 @@ def main():
         "dtype": "%s state, f64 reward, f32 obs/actions" % {1: "u8", 2: "int16", 4: "int32"}[es],
         "data": "synthetic: in-kernel Philox4x32-10 Poisson(5) demand, uniform[-1,1] f32 actions (torch seed 0)",
         "config": {
-            "workload": "C2 shape at the metric's size: MultiAgentInvManagement 4-stage serial "
-                        "(inv_management.py:35-56 constants, MA_1 flags, shared reward), %s envs per GPU, "
-                        "30-period episodes with the reset inside the timed loop"
-                        % ("2^20" if n == 1 << 20 else str(n)),
+            "workload": "%s%s: %s, %s envs per GPU, 30-period episodes with the reset inside the timed loop"
+                        % (args.config, " shape at the metric's size" if args.config == "C2" else "", cdesc,
+                           "2^20" if n == 1 << 20 else str(n)),
             "n_envs_per_gpu": n, "global_envs": world * n, "num_stages": N, "obs_features": F,
             "num_periods": T, "parallelism": "env-sharded x%d (one process per GPU, no data-path collective%s)"
                                              % (world, ", + RCCL all-gather of obs/reward per step" if gather is not None else ""),

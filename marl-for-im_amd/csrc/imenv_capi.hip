@@ -533,9 +533,11 @@ int imenv_create(const ImEnvSpec* spec, int64_t n_envs, int64_t env_offset, int 
   h->es = (size_t)h->host.es;
   const ImEnvSpec& s = *spec;
   const size_t n = n_envs, np = h->host.np, rowb = n * np * h->es;
+  // history rows only when an observation reads an entry older than this step (feature index >= 1)
   bool uses_hist = false;
   for (int f = 0; f < s.num_features; ++f)
-    if (s.feat_group[f] == IMENV_G_DEMAND_HIST || s.feat_group[f] == IMENV_G_ORDER_HIST) uses_hist = true;
+    if ((s.feat_group[f] == IMENV_G_DEMAND_HIST || s.feat_group[f] == IMENV_G_ORDER_HIST) && s.feat_index[f] >= 1)
+      uses_hist = true;
   hipError_t he = hipSetDevice(device);
   if (he != hipSuccess) { delete h; return fail(IMENV_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(he)); }
   char **inv = reinterpret_cast<char**>(&h->d_inv), **bl = reinterpret_cast<char**>(&h->d_bl),

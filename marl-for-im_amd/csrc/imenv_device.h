@@ -359,6 +359,8 @@ struct DynSpec {
   static constexpr int TAB_LDS = IMENV_TABLE_MAX;   // Poisson table staged in LDS
   static constexpr int BS = 256;                     // threads per block
   static constexpr int EPT = 1;                      // envs per thread
+  static constexpr int OBS_ROW = 0;                  // general observation rows are stored directly
+  static constexpr int TD_PRE = 0;                   // in-transit obs slots are loaded after the step
   using ST = ST_;
   const SpecDev* __restrict__ sp;
   const StepArgs& A;
@@ -652,6 +654,13 @@ __device__ __forceinline__ void step_core(const P& p, const int t, const int (&o
 }
 
 // ---------------------------------------------------------------- step body
+// Floats per env of the block's LDS observation slab: the float32 base observation [N][3] (N <= 8),
+// or, for a JIT policy with a general feature list, the whole [N][F] row when N*F <= 48 (OBS_ROW).
+template <class P>
+constexpr int stage_row() {
+  return (P::BASE && P::NT <= 8) ? 3 * P::NT : (!P::BASE ? P::OBS_ROW : 0);
+}
+
 // Structure: (A) issue every load that does not depend on this step's arithmetic (raw words),
 // (B) compute in registers, (C) store; float32 BASE observations are staged through LDS so the
 // block writes its contiguous obs slab with full 1 KiB-per-wave float4 stores.
@@ -667,6 +676,7 @@ struct StepLoad {
   int cdem[P::NT];
   double du[P::NT];
   double macc[4 + P::NT];
+  typename P::ST r_td[P::NT][P::TD_PRE > 0 ? P::TD_PRE : 1];   // in-transit slots of the next obs
 };
 
 template <class P>
@@ -753,6 +763,23 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
 #pragma unroll
       for (int i = 0; i < NT; ++i) if (i < N) du[i] = A.delay_u[((int64_t)t * N + i) * n + el];
     }
+    if constexpr (P::TD_PRE > 0) {
+      // time-dependent observation of period t+1: slot j < d_i - 1 of node i is ring slot
+      // (t + 1 + j) mod d_i, never the slot this step overwrites (t mod d_i), so it loads here with
+      // the state instead of after the step (IM_env.py:416-432)
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+#pragma unroll
+        for (int j = 0; j < P::TD_PRE; ++j) {
+          L.r_td[i][j] = 0;
+          if (i < N) {
+            const int d = p.delay(i);
+            if (j < d - 1 && t + 1 + j - d >= 0)
+              L.r_td[i][j] = p_ring[(int64_t)(p.ring_off(i) + (t + 1 + j) % d) * n + el];
+          }
+        }
+      }
+    }
     if (p.has_metrics() && t > 0) {   // period 0 starts the episode's sums from zero
 #pragma unroll
       for (int k = 0; k < 4 + NT; ++k) if (k < 4 + N) macc[k] = A.metrics[el * (4 + N) + k];
@@ -770,6 +797,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   constexpr int MC = P::MC;
   constexpr bool EXACT = P::EXACT;
   constexpr bool STAGE = P::BASE && NT <= 8;
+  constexpr int OROW = P::BASE ? 0 : P::OBS_ROW;   // general rows staged in LDS (JIT, N*F <= 48)
   using ST = typename P::ST;
   using R = Row<ST, NT, EXACT>;
   using R32 = Row<int32_t, NT, EXACT>;
@@ -802,6 +830,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   const int (&cdem)[NT] = L.cdem;
   const double (&du)[NT] = L.du;
   const double (&macc)[4 + NT] = L.macc;
+  const auto& r_td = L.r_td;
 
   // (A2) random draws depend on no loaded value: placed before the first use of a load, they
   // execute under the loads' latency instead of after the wait
@@ -1037,8 +1066,16 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
         for (int i = 0; i < NT; ++i) {
           const int d = (i < N) ? p.delay(i) : 1;
           v[i] = 0;
-          if (i < N && j < d && tp + j - d >= 0)
-            v[i] = (j == d - 1) ? push[i] : (int)p_ring[(int64_t)(p.ring_off(i) + (tp + j) % d) * n + e];
+          if (i < N && j < d && tp + j - d >= 0) {
+            if (j == d - 1) {
+              v[i] = push[i];
+            } else if constexpr (P::TD_PRE > 0) {
+#pragma unroll
+              for (int q = 0; q < P::TD_PRE; ++q) if (q == j) v[i] = (int)r_td[i][q];
+            } else {
+              v[i] = (int)p_ring[(int64_t)(p.ring_off(i) + (tp + j) % d) * n + e];
+            }
+          }
         }
       } else if (g == IMENV_G_NODE_ID) {
 #pragma unroll
@@ -1049,6 +1086,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
         if (i < N) {
           const int64_t idx = (e * N + i) * F + f;
           if (p.obs_f64()) static_cast<double*>(A.obs)[idx] = p.obs64(g, i, v[i], A.lut64);
+          else if constexpr (OROW > 0) s_obs[tid * OROW + i * F + f] = p.obs32(g, i, v[i], A.lut32);
           else static_cast<float*>(A.obs)[idx] = p.obs32(g, i, v[i], A.lut32);
         }
       }
@@ -1072,7 +1110,7 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   constexpr int NT = P::NT;
   constexpr int BS = P::BS;
   constexpr int EPT = P::EPT;
-  constexpr bool STAGE = P::BASE && NT <= 8;
+  constexpr int SROW = stage_row<P>();   // LDS floats per env (0: observations stored directly)
   const int tid = threadIdx.x;
   const int64_t n = A.n;
   const int64_t eb = (int64_t)blockIdx.x * EPT * BS;
@@ -1082,11 +1120,11 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   for (int k = 0; k < EPT; ++k) step_load(p, A, eb + k * BS + tid, L[k]);
   p.stage_tables(s_tab, poisson);
 #pragma unroll
-  for (int k = 0; k < EPT; ++k) step_finish(p, A, eb + k * BS + tid, L[k], s_tab, s_obs + k * (BS * 3 * NT));
-  if constexpr (P::BASE && STAGE) {
+  for (int k = 0; k < EPT; ++k) step_finish(p, A, eb + k * BS + tid, L[k], s_tab, s_obs + k * (BS * SROW));
+  if constexpr (SROW > 0) {
     if (!p.obs_f64()) {
       __syncthreads();
-      const int row = 3 * p.N();
+      const int row = P::BASE ? 3 * p.N() : SROW;
 #pragma unroll
       for (int k = 0; k < EPT; ++k) {
         const int64_t e0 = eb + k * BS;
@@ -1094,7 +1132,7 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           const int64_t cnt = (n - e0) < BS ? (n - e0) : BS;
           const int64_t total = cnt * row;
           float* gobs = static_cast<float*>(A.obs) + e0 * row;
-          const float* so = s_obs + k * (BS * 3 * NT);
+          const float* so = s_obs + k * (BS * SROW);
           if ((total & 3) == 0) {
             float4* g4 = reinterpret_cast<float4*>(gobs);
             const float4* s4 = reinterpret_cast<const float4*>(so);
@@ -1367,7 +1405,7 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
 // obs staging buffer size (floats) for a policy
 template <class P>
 constexpr int stage_floats() {
-  return (P::BASE && P::NT <= 8) ? P::EPT * P::BS * 3 * P::NT : 4;
+  return stage_row<P>() > 0 ? P::EPT * P::BS * stage_row<P>() : 4;
 }
 
 // Kernel template for any policy whose constructor takes (spec, args).

@@ -151,9 +151,16 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
   const ImEnvSpec& s = d.s;
   const int N = s.num_nodes;
   const int F = s.num_features;
-  bool uses_hist = false;
-  for (int k = 0; k < F; ++k)
-    if (s.feat_group[k] == IMENV_G_DEMAND_HIST || s.feat_group[k] == IMENV_G_ORDER_HIST) uses_hist = true;
+  // history rows are kept only when an observation reads an entry older than this step (index >= 1;
+  // entry 0 is this step's demand / order, in registers); the same rule allocates them (imenv_capi.hip)
+  bool uses_hist = false, has_td = false;
+  for (int k = 0; k < F; ++k) {
+    if ((s.feat_group[k] == IMENV_G_DEMAND_HIST || s.feat_group[k] == IMENV_G_ORDER_HIST) && s.feat_index[k] >= 1)
+      uses_hist = true;
+    if (s.feat_group[k] == IMENV_G_TRANSIT) has_td = true;
+  }
+  // general observation rows of <= 48 floats are staged in LDS and written as contiguous float4 runs
+  const int obs_row = (!base && N * F <= 48) ? N * F : 0;
   const bool inline_tab = d.table_len <= kInlineTable;
   o << "#include \"imenv_device.h\"\n"
        "// generated by imenv_jit.hip: every spec value is a compile-time constant\n"
@@ -167,6 +174,8 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
     << "  static constexpr int BS = " << bs << ";\n"
     << "  static constexpr int EPT = " << ept << ";\n"
     << "  static constexpr int RING = " << d.ring_total << ";\n"
+    << "  static constexpr int OBS_ROW = " << obs_row << ";\n"
+    << "  static constexpr int TD_PRE = " << (has_td && d.dmax > 1 ? d.dmax - 1 : 0) << ";\n"
     << "  using ST = " << (d.es == 1 ? "uint8_t" : d.es == 2 ? "int16_t" : "int32_t") << ";\n"
     << "  const imenv::SpecDev* __restrict__ sp;\n"
     << "  template <class X> __device__ JitSpec(const imenv::SpecDev* __restrict__ s, const X&) : sp(s) {}\n";

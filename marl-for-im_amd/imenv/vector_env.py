@@ -222,6 +222,45 @@ class VectorInvEnv:
         nat.check(self.lib.imenv_state_layout(self._h, byref(eb), byref(rl), byref(rd)), "imenv_state_layout")
         return eb.value, rl.value, rd.value
 
+    def step_traffic(self, action_bytes=4, obs_bytes=4, host_demand=False, metrics=False):
+        """Algorithmic HBM bytes of one step() per env: (steady state, average over an episode).
+
+        The minimal traffic of this handle's layout: actions; inv / backlog / order_u
+        rows read + written (no read at t = 0: the initial state is implicit); node i's arrival read
+        (only once t >= d_i) and departure written; the time-dependent observation's other in-transit
+        slots; int32 noisy-delay carry and divergent backlog_to rows; the demand / order history rows
+        (written every step, read for the features j >= 1); the observation; the reward; optional
+        host-fed demand and harness-metric rows.
+        """
+        es, NP, _ = self.state_layout()
+        s = self.spec
+        N, T = s.num_nodes, s.num_periods
+        d = [int(x) for x in s.delay]
+        split = any(len(c) > 1 for c in s.children)
+        hist = any(g in (nat.G_DEMAND_HIST, nat.G_ORDER_HIST) and j >= 1 for g, j in s.features)
+        per = []
+        for t in range(T):
+            b = N * action_bytes + 3 * NP * es + (3 * NP * es if t > 0 else 0)
+            b += es * sum(1 for i in range(N) if t >= d[i]) + N * es
+            for rows in (s.noisy_delay, split):
+                if rows:
+                    b += 4 * NP + (4 * NP if t > 0 else 0)
+            if hist:
+                b += 2 * NP * es
+            for g, j in s.features:
+                if g in (nat.G_DEMAND_HIST, nat.G_ORDER_HIST) and j >= 1 and t - j >= 0:
+                    b += NP * es
+                elif g == nat.G_TRANSIT:
+                    b += es * sum(1 for i in range(N) if j < d[i] - 1 and t + 1 + j - d[i] >= 0)
+            b += N * s.num_features * obs_bytes
+            b += 8 * N if s.reward_mode == nat.REWARD_INDEPENDENT else 8
+            if host_demand:
+                b += 4 * s.num_retailers
+            if metrics:
+                b += 16 * (4 + N) - (8 * (4 + N) if t == 0 else 0)
+            per.append(b)
+        return per[-1], float(np.mean(per))
+
     def set_jit(self, mode):
         """1: hipRTC kernel specialised for this spec (default); 0: ahead-of-time kernels."""
         nat.check(self.lib.imenv_set_jit(self._h, int(mode)), "imenv_set_jit")
