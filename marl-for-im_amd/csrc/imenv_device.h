@@ -655,10 +655,18 @@ __device__ __forceinline__ void step_core(const P& p, const int t, const int (&o
 
 // ---------------------------------------------------------------- step body
 // Floats per env of the block's LDS observation slab: the float32 base observation [N][3] (N <= 8),
-// or, for a JIT policy with a general feature list, the whole [N][F] row when N*F <= 48 (OBS_ROW).
+// or, for a JIT policy with a general feature list, the whole [N][F] row when the block slab fits
+// 48 KiB (OBS_ROW; imenv_jit.hip picks the block size).
 template <class P>
 constexpr int stage_row() {
   return (P::BASE && P::NT <= 8) ? 3 * P::NT : (!P::BASE ? P::OBS_ROW : 0);
+}
+// LDS floats between consecutive envs of the slab. Each lane writes its own row, so a row length that
+// is a multiple of 8 words puts a wave's writes into 8+ way bank conflicts (64 floats: every lane in
+// one bank); such rows get one pad word and the write-out gathers them back into the packed order.
+template <class P>
+constexpr int stage_stride() {
+  return (stage_row<P>() % 8 == 0 && stage_row<P>() > 0) ? stage_row<P>() + 1 : stage_row<P>();
 }
 
 // Structure: (A) issue every load that does not depend on this step's arithmetic (raw words),
@@ -797,7 +805,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   constexpr int MC = P::MC;
   constexpr bool EXACT = P::EXACT;
   constexpr bool STAGE = P::BASE && NT <= 8;
-  constexpr int OROW = P::BASE ? 0 : P::OBS_ROW;   // general rows staged in LDS (JIT, N*F <= 48)
+  constexpr int OROW = P::BASE ? 0 : P::OBS_ROW;   // general rows staged in LDS (JIT)
   using ST = typename P::ST;
   using R = Row<ST, NT, EXACT>;
   using R32 = Row<int32_t, NT, EXACT>;
@@ -999,7 +1007,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   // MAIM_div_env.py:343-439)
   if constexpr (P::BASE) {
     if (STAGE && !p.obs_f64()) {
-      const int row = 3 * N;
+      constexpr int row = stage_stride<P>();
       if (valid) {
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
@@ -1086,7 +1094,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
         if (i < N) {
           const int64_t idx = (e * N + i) * F + f;
           if (p.obs_f64()) static_cast<double*>(A.obs)[idx] = p.obs64(g, i, v[i], A.lut64);
-          else if constexpr (OROW > 0) s_obs[tid * OROW + i * F + f] = p.obs32(g, i, v[i], A.lut32);
+          else if constexpr (OROW > 0) s_obs[tid * stage_stride<P>() + i * F + f] = p.obs32(g, i, v[i], A.lut32);
           else static_cast<float*>(A.obs)[idx] = p.obs32(g, i, v[i], A.lut32);
         }
       }
@@ -1119,26 +1127,34 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
 #pragma unroll
   for (int k = 0; k < EPT; ++k) step_load(p, A, eb + k * BS + tid, L[k]);
   p.stage_tables(s_tab, poisson);
+  constexpr int SSTR = stage_stride<P>();
 #pragma unroll
-  for (int k = 0; k < EPT; ++k) step_finish(p, A, eb + k * BS + tid, L[k], s_tab, s_obs + k * (BS * SROW));
+  for (int k = 0; k < EPT; ++k) step_finish(p, A, eb + k * BS + tid, L[k], s_tab, s_obs + k * (BS * SSTR));
   if constexpr (SROW > 0) {
+    // (staged rows: SROW == 3 N for the base layout, as N == NT whenever it is staged)
     if (!p.obs_f64()) {
       __syncthreads();
-      const int row = P::BASE ? 3 * p.N() : SROW;
+      constexpr int row = SROW;
+      auto at = [](const float* so, int q) { return so[(q / row) * SSTR + q % row]; };   // packed -> slab
 #pragma unroll
       for (int k = 0; k < EPT; ++k) {
         const int64_t e0 = eb + k * BS;
         if (e0 < n) {
-          const int64_t cnt = (n - e0) < BS ? (n - e0) : BS;
-          const int64_t total = cnt * row;
+          const int cnt = (n - e0) < BS ? (int)(n - e0) : BS;
+          const int total = cnt * row;
           float* gobs = static_cast<float*>(A.obs) + e0 * row;
-          const float* so = s_obs + k * (BS * SROW);
+          const float* so = s_obs + k * (BS * SSTR);
           if ((total & 3) == 0) {
             float4* g4 = reinterpret_cast<float4*>(gobs);
-            const float4* s4 = reinterpret_cast<const float4*>(so);
-            for (int64_t q = tid; q < total / 4; q += BS) g4[q] = s4[q];
+            if constexpr (SSTR == row) {
+              const float4* s4 = reinterpret_cast<const float4*>(so);
+              for (int q = tid; q < total / 4; q += BS) g4[q] = s4[q];
+            } else {
+              for (int q = tid; q < total / 4; q += BS)
+                g4[q] = make_float4(at(so, 4 * q), at(so, 4 * q + 1), at(so, 4 * q + 2), at(so, 4 * q + 3));
+            }
           } else {
-            for (int64_t q = tid; q < total; q += BS) gobs[q] = so[q];
+            for (int q = tid; q < total; q += BS) gobs[q] = at(so, q);
           }
         }
       }
@@ -1405,7 +1421,7 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
 // obs staging buffer size (floats) for a policy
 template <class P>
 constexpr int stage_floats() {
-  return stage_row<P>() > 0 ? P::EPT * P::BS * stage_row<P>() : 4;
+  return stage_row<P>() > 0 ? P::EPT * P::BS * stage_stride<P>() : 4;
 }
 
 // Kernel template for any policy whose constructor takes (spec, args).

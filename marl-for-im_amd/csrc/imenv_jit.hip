@@ -67,6 +67,27 @@ int jit_block_size() {
   return bs;
 }
 
+// General observation rows (not the base [N][3] layout) are staged in LDS when a block's slab fits
+// kStageLds bytes: the block size halves (256 -> 128 -> 64, unless IMENV_JIT_BS is set) until it does,
+// so wide rows (8 stages with in-transit features, 2-level trees with shared-network ids) keep
+// coalesced float4 stores at 4+ waves per SIMD instead of falling back to strided scalar stores.
+constexpr int kStageLds = 48 * 1024;
+
+int general_row(const SpecDev& d, bool base) { return base ? 0 : d.s.num_nodes * d.s.num_features; }
+
+int jit_step_block_size(const SpecDev& d, bool base) {
+  int bs = jit_block_size();
+  const int row = general_row(d, base);
+  if (row > 0 && !std::getenv("IMENV_JIT_BS"))
+    while (bs > 64 && bs * row * 4 > kStageLds) bs /= 2;
+  return bs;
+}
+
+int jit_obs_row(const SpecDev& d, bool base, int bs) {
+  const int row = general_row(d, base);
+  return (row > 0 && bs * row * 4 <= kStageLds) ? row : 0;
+}
+
 // Envs per thread of the JIT step kernel (step_body). 1: with two envs per thread the footprint probe
 // gets 5% faster (tools/probe3.py: 19.35 vs 20.42 us at C2 size), but the real kernel gets slower
 // (23.4 vs 21.0 us: twice the registers, a 24 KiB obs slab per block), profiles/r01/probe3_u8_floor.log.
@@ -159,8 +180,8 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
       uses_hist = true;
     if (s.feat_group[k] == IMENV_G_TRANSIT) has_td = true;
   }
-  // general observation rows of <= 48 floats are staged in LDS and written as contiguous float4 runs
-  const int obs_row = (!base && N * F <= 48) ? N * F : 0;
+  // general observation rows staged in LDS and written as contiguous float4 runs (jit_obs_row)
+  const int obs_row = jit_obs_row(d, base, bs);
   const bool inline_tab = d.table_len <= kInlineTable;
   o << "#include \"imenv_device.h\"\n"
        "// generated by imenv_jit.hip: every spec value is a compile-time constant\n"
@@ -264,7 +285,7 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
 
 std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f) {
   std::ostringstream o;
-  emit_policy(o, d, maxc, base, f, jit_block_size(), jit_envs_per_thread(d, base));
+  emit_policy(o, d, maxc, base, f, jit_step_block_size(d, base), jit_envs_per_thread(d, base));
   o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
        "imenv_step_jit(const imenv::SpecDev* __restrict__ sp, const imenv::StepArgs A) {\n"
        "  __shared__ uint32_t s_tab[JitSpec::TAB_LDS];\n"
@@ -370,7 +391,7 @@ bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const st
               std::string& msg) {
   const std::string src = jit_source(d, maxc, base, f);
   if (!load_module(src, arch, "imenv_step_jit", out, msg)) return false;
-  out.bs = jit_block_size();
+  out.bs = jit_step_block_size(d, base);
   out.ept = jit_envs_per_thread(d, base);
   char tag[160];
   std::snprintf(tag, sizeof tag, "jit:imenv_step_jit[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,ept=%d,%zuB]",

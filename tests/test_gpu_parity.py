@@ -268,3 +268,42 @@ def test_gpu_two_envs_per_thread_variant(name, kernel_mode, monkeypatch):
     np.testing.assert_array_equal(out["obs"], d["obs"].astype(np.float32))
     for k in ("inv", "backlog", "order_u"):
         np.testing.assert_array_equal(out[k].astype(np.float64), d[k])
+
+
+@pytest.mark.parametrize("kind,cfg", [("MAIM", C2), ("IM", C3), ("MAIM_div", C4),
+                                      ("IM", dict(C2, time_dependency=True, prev_demand=True, prev_actions=True,
+                                                  prev_length=2))])
+def test_gpu_ragged_env_counts(kind, cfg):
+    """Env counts that fill no block exactly (1, 3, 255, 257, 1000: tail lanes, partial LDS obs slabs
+    whose float count is not a multiple of 4) == oracle, float32 obs and actions, in-kernel draws."""
+    for n in (1, 3, 255, 257, 1000):
+        env = _env(kind, cfg, n, env_offset=77)
+        ora = OracleEnv(kind, cfg, n_envs=n)
+        o_g = env.reset()
+        o_c = ora.reset(rng=dict(seed=52, episode=0, env_offset=77, mu=5))
+        np.testing.assert_array_equal(o_g.cpu().numpy(), o_c.astype(np.float32))
+        rs = np.random.RandomState(n)
+        for t in range(30):
+            a32 = rs.uniform(-1, 1, size=(n, env.N)).astype(np.float32)
+            o_g, r_g, d_g, _ = env.step(torch.as_tensor(a32, device=DEV))
+            o_c, r_c, d_c, _ = ora.step(a32.astype(np.float64))
+            np.testing.assert_array_equal(o_g.cpu().numpy(), o_c.astype(np.float32), err_msg="n=%d t=%d" % (n, t))
+            np.testing.assert_array_equal(r_g.cpu().numpy(), r_c, err_msg="n=%d t=%d" % (n, t))
+            st = env.state()
+            for k in ("inv", "backlog", "order_u"):
+                np.testing.assert_array_equal(st[k].cpu().numpy(), ora.state_arrays()[k])
+        env.close()
+
+
+def test_gpu_step_traffic_matches_bench_formula():
+    """Algorithmic bytes per env-step for the bench layouts: C2 104 B steady,
+    103.367 B averaged over the 30-period episode."""
+    env = _env("MAIM", C2, 64)
+    assert env.state_layout()[0] == 1
+    steady, avg = env.step_traffic()
+    assert steady == 104 and abs(avg - (104 - 19 / 30)) < 1e-9
+    env.close()
+    env = _env("MAIM_div", C4, 64)     # td slot of node 1 (delay 2), backlog_to rows, no history rows
+    steady, _ = env.step_traffic()
+    assert steady == 16 + 24 + 4 + 1 + 4 + 32 + 96 + 8
+    env.close()
