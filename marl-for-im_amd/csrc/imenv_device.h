@@ -360,6 +360,7 @@ struct DynSpec {
   static constexpr int BS = 256;                     // threads per block
   static constexpr int EPT = 1;                      // envs per thread
   static constexpr int OBS_ROW = 0;                  // general observation rows are stored directly
+  static constexpr bool OBS_STAGE64 = false;         // float64 observations are stored directly
   static constexpr int TD_PRE = 0;                   // in-transit obs slots are loaded after the step
   using ST = ST_;
   const SpecDev* __restrict__ sp;
@@ -654,19 +655,26 @@ __device__ __forceinline__ void step_core(const P& p, const int t, const int (&o
 }
 
 // ---------------------------------------------------------------- step body
-// Floats per env of the block's LDS observation slab: the float32 base observation [N][3] (N <= 8),
-// or, for a JIT policy with a general feature list, the whole [N][F] row when the block slab fits
-// 48 KiB (OBS_ROW; imenv_jit.hip picks the block size).
+// Observation values per env of the block's LDS slab: the base observation [N][3] (N <= 8), or, for a
+// JIT policy with a general feature list, the whole [N][F] row when the block slab fits 48 KiB
+// (OBS_ROW; imenv_jit.hip picks the block size). Values are float32, or float64 for a JIT policy
+// specialised for float64 observations (OBS_STAGE64); the AOT kernels stage float32 only.
 template <class P>
 constexpr int stage_row() {
   return (P::BASE && P::NT <= 8) ? 3 * P::NT : (!P::BASE ? P::OBS_ROW : 0);
 }
-// LDS floats between consecutive envs of the slab. Each lane writes its own row, so a row length that
-// is a multiple of 8 words puts a wave's writes into 8+ way bank conflicts (64 floats: every lane in
-// one bank); such rows get one pad word and the write-out gathers them back into the packed order.
+// Values between consecutive envs of the slab. Each lane writes its own row, so a row of a multiple of
+// 8 floats (or an even number of doubles) puts a wave's writes into bank conflicts (64 floats: every
+// lane in one bank); such rows get one pad value and the write-out gathers them back into packed order.
 template <class P>
 constexpr int stage_stride() {
-  return (stage_row<P>() % 8 == 0 && stage_row<P>() > 0) ? stage_row<P>() + 1 : stage_row<P>();
+  return (stage_row<P>() > 0 && stage_row<P>() % (P::OBS_STAGE64 ? 2 : 8) == 0) ? stage_row<P>() + 1
+                                                                                 : stage_row<P>();
+}
+// Whether this call's observations go through the slab (the slab's value type matches the call's).
+template <class P>
+__device__ __forceinline__ bool staged_obs(const P& p) {
+  return P::OBS_STAGE64 ? p.obs_f64() : !p.obs_f64();
 }
 
 // Structure: (A) issue every load that does not depend on this step's arithmetic (raw words),
@@ -1006,15 +1014,22 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   // observation for period t+1 (IM_env.py:231-285, MAIM_env.py:242-328, IM_div_env.py:304-359,
   // MAIM_div_env.py:343-439)
   if constexpr (P::BASE) {
-    if (STAGE && !p.obs_f64()) {
+    if (STAGE && staged_obs(p)) {
       constexpr int row = stage_stride<P>();
       if (valid) {
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
           if (i < N) {
-            s_obs[tid * row + 3 * i + 0] = p.obs32(IMENV_G_INV, i, inv[i], A.lut32);
-            s_obs[tid * row + 3 * i + 1] = p.obs32(IMENV_G_BACKLOG, i, bl[i], A.lut32);
-            s_obs[tid * row + 3 * i + 2] = p.obs32(IMENV_G_ORDER_U, i, ou[i], A.lut32);
+            if constexpr (P::OBS_STAGE64) {
+              double* sd = reinterpret_cast<double*>(s_obs);
+              sd[tid * row + 3 * i + 0] = p.obs64(IMENV_G_INV, i, inv[i], A.lut64);
+              sd[tid * row + 3 * i + 1] = p.obs64(IMENV_G_BACKLOG, i, bl[i], A.lut64);
+              sd[tid * row + 3 * i + 2] = p.obs64(IMENV_G_ORDER_U, i, ou[i], A.lut64);
+            } else {
+              s_obs[tid * row + 3 * i + 0] = p.obs32(IMENV_G_INV, i, inv[i], A.lut32);
+              s_obs[tid * row + 3 * i + 1] = p.obs32(IMENV_G_BACKLOG, i, bl[i], A.lut32);
+              s_obs[tid * row + 3 * i + 2] = p.obs32(IMENV_G_ORDER_U, i, ou[i], A.lut32);
+            }
           }
         }
       }
@@ -1093,9 +1108,16 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
       for (int i = 0; i < NT; ++i) {
         if (i < N) {
           const int64_t idx = (e * N + i) * F + f;
-          if (p.obs_f64()) static_cast<double*>(A.obs)[idx] = p.obs64(g, i, v[i], A.lut64);
-          else if constexpr (OROW > 0) s_obs[tid * stage_stride<P>() + i * F + f] = p.obs32(g, i, v[i], A.lut32);
-          else static_cast<float*>(A.obs)[idx] = p.obs32(g, i, v[i], A.lut32);
+          if (p.obs_f64()) {
+            if constexpr (OROW > 0 && P::OBS_STAGE64)
+              reinterpret_cast<double*>(s_obs)[tid * stage_stride<P>() + i * F + f] = p.obs64(g, i, v[i], A.lut64);
+            else
+              static_cast<double*>(A.obs)[idx] = p.obs64(g, i, v[i], A.lut64);
+          } else if constexpr (OROW > 0 && !P::OBS_STAGE64) {
+            s_obs[tid * stage_stride<P>() + i * F + f] = p.obs32(g, i, v[i], A.lut32);
+          } else {
+            static_cast<float*>(A.obs)[idx] = p.obs32(g, i, v[i], A.lut32);
+          }
         }
       }
     };
@@ -1128,11 +1150,35 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   for (int k = 0; k < EPT; ++k) step_load(p, A, eb + k * BS + tid, L[k]);
   p.stage_tables(s_tab, poisson);
   constexpr int SSTR = stage_stride<P>();
+  constexpr int SLAB = BS * SSTR * (P::OBS_STAGE64 ? 2 : 1);   // floats per BS-env slab
 #pragma unroll
-  for (int k = 0; k < EPT; ++k) step_finish(p, A, eb + k * BS + tid, L[k], s_tab, s_obs + k * (BS * SSTR));
-  if constexpr (SROW > 0) {
+  for (int k = 0; k < EPT; ++k) step_finish(p, A, eb + k * BS + tid, L[k], s_tab, s_obs + k * SLAB);
+  if constexpr (SROW > 0 && P::OBS_STAGE64) {
+    // float64 rows: the same write-out in 16-byte double2 runs
+    if (staged_obs(p)) {
+      __syncthreads();
+      constexpr int row = SROW;
+      auto at = [](const double* so, int q) { return so[(q / row) * SSTR + q % row]; };
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) {
+        const int64_t e0 = eb + k * BS;
+        if (e0 < n) {
+          const int cnt = (n - e0) < BS ? (int)(n - e0) : BS;
+          const int total = cnt * row;
+          double* gobs = static_cast<double*>(A.obs) + e0 * row;
+          const double* so = reinterpret_cast<const double*>(s_obs + k * SLAB);
+          if ((total & 1) == 0) {
+            double2* g2 = reinterpret_cast<double2*>(gobs);
+            for (int q = tid; q < total / 2; q += BS) g2[q] = make_double2(at(so, 2 * q), at(so, 2 * q + 1));
+          } else {
+            for (int q = tid; q < total; q += BS) gobs[q] = at(so, q);
+          }
+        }
+      }
+    }
+  } else if constexpr (SROW > 0) {
     // (staged rows: SROW == 3 N for the base layout, as N == NT whenever it is staged)
-    if (!p.obs_f64()) {
+    if (staged_obs(p)) {
       __syncthreads();
       constexpr int row = SROW;
       auto at = [](const float* so, int q) { return so[(q / row) * SSTR + q % row]; };   // packed -> slab
@@ -1143,7 +1189,7 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           const int cnt = (n - e0) < BS ? (int)(n - e0) : BS;
           const int total = cnt * row;
           float* gobs = static_cast<float*>(A.obs) + e0 * row;
-          const float* so = s_obs + k * (BS * SSTR);
+          const float* so = s_obs + k * SLAB;
           if ((total & 3) == 0) {
             float4* g4 = reinterpret_cast<float4*>(gobs);
             if constexpr (SSTR == row) {
@@ -1421,7 +1467,7 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
 // obs staging buffer size (floats) for a policy
 template <class P>
 constexpr int stage_floats() {
-  return stage_row<P>() > 0 ? P::EPT * P::BS * stage_stride<P>() : 4;
+  return stage_row<P>() > 0 ? P::EPT * P::BS * stage_stride<P>() * (P::OBS_STAGE64 ? 2 : 1) : 4;
 }
 
 // Kernel template for any policy whose constructor takes (spec, args).

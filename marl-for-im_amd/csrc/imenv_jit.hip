@@ -71,31 +71,32 @@ int jit_block_size() {
 // kStageLds bytes: the block size halves (256 -> 128 -> 64, unless IMENV_JIT_BS is set) until it does,
 // so wide rows (8 stages with in-transit features, 2-level trees with shared-network ids) keep
 // coalesced float4 stores at 4+ waves per SIMD instead of falling back to strided scalar stores.
+// vbytes: 4 (float32 observations) or 8 (float64, staged as doubles).
 constexpr int kStageLds = 48 * 1024;
 
 int general_row(const SpecDev& d, bool base) { return base ? 0 : d.s.num_nodes * d.s.num_features; }
 
-int jit_step_block_size(const SpecDev& d, bool base) {
+int jit_step_block_size(const SpecDev& d, bool base, int vbytes) {
   int bs = jit_block_size();
   const int row = general_row(d, base);
   if (row > 0 && !std::getenv("IMENV_JIT_BS"))
-    while (bs > 64 && bs * row * 4 > kStageLds) bs /= 2;
+    while (bs > 64 && bs * row * vbytes > kStageLds) bs /= 2;
   return bs;
 }
 
-int jit_obs_row(const SpecDev& d, bool base, int bs) {
+int jit_obs_row(const SpecDev& d, bool base, int bs, int vbytes) {
   const int row = general_row(d, base);
-  return (row > 0 && bs * row * 4 <= kStageLds) ? row : 0;
+  return (row > 0 && bs * row * vbytes <= kStageLds) ? row : 0;
 }
 
 // Envs per thread of the JIT step kernel (step_body). 1: with two envs per thread the footprint probe
 // gets 5% faster (tools/probe3.py: 19.35 vs 20.42 us at C2 size), but the real kernel gets slower
 // (23.4 vs 21.0 us: twice the registers, a 24 KiB obs slab per block), profiles/r01/probe3_u8_floor.log.
-// IMENV_JIT_EPT=2 selects it (only for the staged base-observation layout, N <= 8).
-int jit_envs_per_thread(const SpecDev& d, bool base) {
+// IMENV_JIT_EPT=2 selects it (only for the staged float32 base-observation layout, N <= 8).
+int jit_envs_per_thread(const SpecDev& d, bool base, bool obs_f64) {
   int ept = 1;
   if (const char* v = std::getenv("IMENV_JIT_EPT")) ept = std::atoi(v) == 2 ? 2 : 1;
-  if (!(base && d.s.num_nodes <= 8)) ept = 1;
+  if (!(base && d.s.num_nodes <= 8) || obs_f64) ept = 1;
   return ept;
 }
 
@@ -147,11 +148,18 @@ void emit_obs_hooks(std::ostream& o, const SpecDev& d) {
       }
       const std::string guard = "if ((unsigned)v <= " + std::to_string(mx) + "u) return ";
       const std::string cs = "    case " + std::to_string(g * 256 + i) + ": ";
+      // no verified closed form: the reference expression itself (IEEE double division: exact for every
+      // v), not a table gather (a dependent gather per value made float64 observations 4-10x slower)
+      const std::string direct = "imenv::obs_map(" + std::to_string(mode) + ", (double)v, " + dlit(s.a) + ", " +
+                                 dlit(s.b - s.a) + ", " + dlit(s.group_den[g][i]) + ", " +
+                                 dlit(s.group_clip[g][i]) + ")";
       if (k1) c32 << cs << guard << "__builtin_fmaf((float)v, " << flit(c1) << ", " << flit(c0) << "); break;\n";
       else if (k2) c32 << cs << guard << "(float)__builtin_fma((double)v, " << dlit(d1) << ", " << dlit(s.a) << "); break;\n";
       else if (k3) c32 << cs << guard << "(float)((double)v * " << dlit(d1) << " + " << dlit(s.a) << "); break;\n";
+      else c32 << cs << "return (float)" << direct << ";\n";
       if (q1) c64 << cs << guard << "__builtin_fma((double)v, " << dlit(d1) << ", " << dlit(s.a) << "); break;\n";
       else if (q2) c64 << cs << guard << "(double)v * " << dlit(d1) << " + " << dlit(s.a) << "; break;\n";
+      else c64 << cs << "return " << direct << ";\n";
     }
   }
   o << "  __device__ float obs32(int g, int i, int v, const float* __restrict__ lut) const {\n"
@@ -180,8 +188,8 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
       uses_hist = true;
     if (s.feat_group[k] == IMENV_G_TRANSIT) has_td = true;
   }
-  // general observation rows staged in LDS and written as contiguous float4 runs (jit_obs_row)
-  const int obs_row = jit_obs_row(d, base, bs);
+  // general observation rows staged in LDS and written as contiguous float4 / double2 runs (jit_obs_row)
+  const int obs_row = jit_obs_row(d, base, bs, f.obs_f64 ? 8 : 4);
   const bool inline_tab = d.table_len <= kInlineTable;
   o << "#include \"imenv_device.h\"\n"
        "// generated by imenv_jit.hip: every spec value is a compile-time constant\n"
@@ -196,6 +204,7 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
     << "  static constexpr int EPT = " << ept << ";\n"
     << "  static constexpr int RING = " << d.ring_total << ";\n"
     << "  static constexpr int OBS_ROW = " << obs_row << ";\n"
+    << "  static constexpr bool OBS_STAGE64 = " << blit(f.obs_f64) << ";\n"
     << "  static constexpr int TD_PRE = " << (has_td && d.dmax > 1 ? d.dmax - 1 : 0) << ";\n"
     << "  using ST = " << (d.es == 1 ? "uint8_t" : d.es == 2 ? "int16_t" : "int32_t") << ";\n"
     << "  const imenv::SpecDev* __restrict__ sp;\n"
@@ -285,7 +294,8 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
 
 std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f) {
   std::ostringstream o;
-  emit_policy(o, d, maxc, base, f, jit_step_block_size(d, base), jit_envs_per_thread(d, base));
+  emit_policy(o, d, maxc, base, f, jit_step_block_size(d, base, f.obs_f64 ? 8 : 4),
+              jit_envs_per_thread(d, base, f.obs_f64));
   o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
        "imenv_step_jit(const imenv::SpecDev* __restrict__ sp, const imenv::StepArgs A) {\n"
        "  __shared__ uint32_t s_tab[JitSpec::TAB_LDS];\n"
@@ -391,8 +401,8 @@ bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const st
               std::string& msg) {
   const std::string src = jit_source(d, maxc, base, f);
   if (!load_module(src, arch, "imenv_step_jit", out, msg)) return false;
-  out.bs = jit_step_block_size(d, base);
-  out.ept = jit_envs_per_thread(d, base);
+  out.bs = jit_step_block_size(d, base, f.obs_f64 ? 8 : 4);
+  out.ept = jit_envs_per_thread(d, base, f.obs_f64);
   char tag[160];
   std::snprintf(tag, sizeof tag, "jit:imenv_step_jit[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,ept=%d,%zuB]",
                 d.s.num_nodes, maxc, base ? 1 : 0, d.es, f.key(), out.bs, out.ept, src.size());

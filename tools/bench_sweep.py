@@ -4,7 +4,7 @@ observation-flag combinations the reference's scripts use), not only the bench w
 
     python tools/bench_sweep.py [--n-envs 1048576] [--out gpurun_out/sweep.jsonl]
 
-Per config: float32 actions and observations, in-kernel Philox demand (and noisy delay where the case
+Per config: float32 actions, float32 observations (--obs-f64: float64), in-kernel Philox demand (and noisy delay where the case
 has it), 2 warmup + 2 timed episodes; the step kernel is timed with HIP events on its stream over
 launches t = 1..T-1 of each timed episode. achieved = VectorInvEnv.step_traffic() bytes x n / time.
 One JSON line per config.
@@ -27,7 +27,7 @@ from golden_io import case_names, load_case  # noqa: E402
 HBM_PEAK_GBS = 8000.0
 
 
-def run_case(name, n, dev):
+def run_case(name, n, dev, obs_dtype=torch.float32):
     from imenv import VectorInvEnv
     meta, _ = load_case(name)
     env = VectorInvEnv(meta["kind"], meta["config"], n_envs=n, device=dev)
@@ -36,7 +36,7 @@ def run_case(name, n, dev):
     g = torch.Generator(device=dev)
     g.manual_seed(0)
     acts = torch.rand((T, n, N), generator=g, device=dev) * 2 - 1
-    obs = torch.empty((n, N, env.F), dtype=torch.float32, device=dev)
+    obs = torch.empty((n, N, env.F), dtype=obs_dtype, device=dev)
     rew = torch.empty(env.reward_shape(), dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
     times = []
@@ -54,9 +54,9 @@ def run_case(name, n, dev):
             e1.synchronize()
             times.append(e0.elapsed_time(e1) / (T - 1))
     us = float(np.mean(times)) * 1e3
-    steady, avg = env.step_traffic()
+    steady, avg = env.step_traffic(obs_bytes=obs.element_size())
     gbs = avg * n / (us * 1e-6) / 1e9
-    out = dict(case=name, kind=meta["kind"], N=N, F=env.F, state_bytes=env.state_layout()[0],
+    out = dict(case=name, kind=meta["kind"], N=N, F=env.F, obs=str(obs_dtype).split(".")[-1], state_bytes=env.state_layout()[0],
                reward=("independent" if env.spec.reward_mode == 2 else "scalar"), noisy_delay=noisy,
                n_envs=n, kernel_us=round(us, 3), env_steps_per_s=round(n / (us * 1e-6), 1),
                bytes_per_env_step=round(avg, 3), achieved_gbs=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4),
@@ -70,13 +70,14 @@ def main():
     ap.add_argument("--n-envs", type=int, default=1 << 20)
     ap.add_argument("--out", default=None)
     ap.add_argument("--cases", default=None, help="comma-separated subset")
+    ap.add_argument("--obs-f64", action="store_true", help="float64 observations (the reference's dtype)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     names = args.cases.split(",") if args.cases else case_names()
     fo = open(args.out, "w") if args.out else None
     for name in names:
-        r = run_case(name, args.n_envs, dev)
+        r = run_case(name, args.n_envs, dev, torch.float64 if args.obs_f64 else torch.float32)
         line = json.dumps(r)
         print(line, flush=True)
         if fo:
