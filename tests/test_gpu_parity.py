@@ -270,24 +270,32 @@ def test_gpu_two_envs_per_thread_variant(name, kernel_mode, monkeypatch):
         np.testing.assert_array_equal(out[k].astype(np.float64), d[k])
 
 
-@pytest.mark.parametrize("kind,cfg", [("MAIM", C2), ("IM", C3), ("MAIM_div", C4),
+C2_3 = dict(C2, num_stages=3, init_inv=np.ones(3) * 10, inv_target=np.zeros(3), inv_max=np.ones(3) * 30,
+            price=np.array([4, 3, 2, 1]), stock_cost=np.array([0.35, 0.3, 0.4]),
+            backlog_cost=np.array([0.5, 0.7, 0.6]), delay=np.array([1, 2, 3]))
+
+
+@pytest.mark.parametrize("kind,cfg", [("MAIM", C2), ("IM", C3), ("MAIM_div", C4), ("MAIM", C2_3),
                                       ("IM", dict(C2, time_dependency=True, prev_demand=True, prev_actions=True,
                                                   prev_length=2))])
-def test_gpu_ragged_env_counts(kind, cfg):
+@pytest.mark.parametrize("odt", [torch.float32, torch.float64])
+def test_gpu_ragged_env_counts(kind, cfg, odt):
     """Env counts that fill no block exactly (1, 3, 255, 257, 1000: tail lanes, partial LDS obs slabs
-    whose float count is not a multiple of 4) == oracle, float32 obs and actions, in-kernel draws."""
+    whose value count is not a multiple of the float4 / double2 run; 3 stages: odd base rows) == oracle,
+    float32 actions, float32 / float64 observations, in-kernel draws."""
+    cast = (lambda x: x.astype(np.float32)) if odt == torch.float32 else (lambda x: x)
     for n in (1, 3, 255, 257, 1000):
-        env = _env(kind, cfg, n, env_offset=77)
+        env = _env(kind, cfg, n, env_offset=77, obs_dtype=odt)
         ora = OracleEnv(kind, cfg, n_envs=n)
         o_g = env.reset()
         o_c = ora.reset(rng=dict(seed=52, episode=0, env_offset=77, mu=5))
-        np.testing.assert_array_equal(o_g.cpu().numpy(), o_c.astype(np.float32))
+        np.testing.assert_array_equal(o_g.cpu().numpy(), cast(o_c))
         rs = np.random.RandomState(n)
         for t in range(30):
             a32 = rs.uniform(-1, 1, size=(n, env.N)).astype(np.float32)
             o_g, r_g, d_g, _ = env.step(torch.as_tensor(a32, device=DEV))
             o_c, r_c, d_c, _ = ora.step(a32.astype(np.float64))
-            np.testing.assert_array_equal(o_g.cpu().numpy(), o_c.astype(np.float32), err_msg="n=%d t=%d" % (n, t))
+            np.testing.assert_array_equal(o_g.cpu().numpy(), cast(o_c), err_msg="n=%d t=%d" % (n, t))
             np.testing.assert_array_equal(r_g.cpu().numpy(), r_c, err_msg="n=%d t=%d" % (n, t))
             st = env.state()
             for k in ("inv", "backlog", "order_u"):
