@@ -178,6 +178,13 @@ __device__ __forceinline__ uint32_t rng_word(uint32_t gid, uint32_t ep, int t, u
                                              uint32_t k1) {
   return word_of(rng_block(gid, ep, t, stream, lane, k0, k1), t & 3);
 }
+// Noisy delay draws one word per node per period: word i mod 4 of Philox(counter = (gid, ep, t,
+// STREAM_NOISY_DELAY << 16 | i / 4)), so one block serves four nodes of the same period and a
+// one-period kernel (the step kernel) pays one block per four nodes instead of one per node.
+__device__ __forceinline__ uint4 rng_node_block(uint32_t gid, uint32_t ep, int t, uint32_t stream, int group,
+                                                uint32_t k0, uint32_t k1) {
+  return philox4(gid, ep, (uint32_t)t, (stream << 16) | (uint32_t)group, k0, k1);
+}
 
 // ceil(a / b) for a > 0, 1 <= b <= 8 (b = number of eligible children): the common b = 1, 2 without
 // an integer division
@@ -852,6 +859,14 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   // execute under the loads' latency instead of after the wait
   int cdraw[NT];
   bool nd_double[NT], nd_zero[NT], nd_delay[NT];
+  constexpr int NG = (NT + 3) / 4;
+  uint4 dblk[NG];   // noisy delay: one block per four nodes (rng_node_block)
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    dblk[g] = make_uint4(0u, 0u, 0u, 0u);
+    if (p.noisy_delay() && !p.has_delay_u() && 4 * g < N)
+      dblk[g] = rng_node_block(gid, ep, t, STREAM_NOISY_DELAY, g, k0, k1);
+  }
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     cdraw[i] = 0;
@@ -876,7 +891,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
         }
       }
       if (p.noisy_delay() && !p.has_delay_u() && t >= p.delay(i))
-        nd_delay[i] = (uint64_t)rng_word(gid, ep, t, STREAM_NOISY_DELAY, i, k0, k1) < A.noisy_delay_thr32;
+        nd_delay[i] = (uint64_t)word_of(dblk[i >> 2], i & 3) < A.noisy_delay_thr32;
     }
   }
 
@@ -1315,7 +1330,8 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
       if (i < N)
         for (int k = 0; k < p.delay(i); ++k) s_ring[(p.ring_off(i) + k) * BS + tid] = 0;
 
-    uint4 rb_dem[NT], rb_dbl[NT], rb_zero[NT], rb_delay[NT];   // one Philox block per 4 periods
+    uint4 rb_dem[NT], rb_dbl[NT], rb_zero[NT];   // one Philox block per 4 periods
+    uint4 rb_delay[(NT + 3) / 4];                 // noisy delay: one block per 4 nodes per period
 #pragma unroll 1
     for (int t = 0; t < T; ++t) {
       const int tw = t & 3;
@@ -1332,10 +1348,10 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
           }
         }
       }
-      if (tw == 0 && p.noisy_delay()) {
+      if (p.noisy_delay()) {
 #pragma unroll
-        for (int i = 0; i < NT; ++i)
-          if (i < N) rb_delay[i] = rng_block(gid, ep, t, STREAM_NOISY_DELAY, i, k0, k1);
+        for (int g = 0; g < (NT + 3) / 4; ++g)
+          if (4 * g < N) rb_delay[g] = rng_node_block(gid, ep, t, STREAM_NOISY_DELAY, g, k0, k1);
       }
       int cust[NT], arr[NT], order[NT];
       bool defer[NT];
@@ -1370,7 +1386,7 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
           }
           const int d = p.delay(i);
           if (t >= d) arr[i] = s_ring[(p.ring_off(i) + t % d) * BS + tid];
-          if (p.noisy_delay() && t >= d) defer[i] = (uint64_t)word_of(rb_delay[i], tw) < A.noisy_delay_thr32;
+          if (p.noisy_delay() && t >= d) defer[i] = (uint64_t)word_of(rb_delay[i >> 2], i & 3) < A.noisy_delay_thr32;
           // base_stock_policy (base_restock_policy.py:12-20): order up to lvl from the echelon position
           // inv + order_u - backlog (integers: exact, as the reference's float64 sum of integers),
           // min(order_max, max(policy - position, 0)); then the env's decode

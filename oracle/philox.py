@@ -20,7 +20,9 @@ in tests/test_oracle_golden.py (KAT tests).
 Counter layout used by the product (all uint32):
     c0 = global env id, c1 = episode, c2 = period t // 4, c3 = (stream << 16) | lane
 and the word for period t is output word t % 4, so one Philox block serves four consecutive
-periods (lane = retailer row for demand draws, node for noisy delay).
+periods (lane = retailer row, for demand and noisy-demand draws). Noisy delay (one word per node
+per period) uses c2 = t, c3 = (stream << 16) | node // 4 and output word node % 4: one block
+serves four nodes of one period (``node_word``).
 Key: (seed & 0xffffffff, seed >> 32).
 """
 import numpy as np
@@ -68,6 +70,12 @@ def stream_word(gid, ep, t, stream, lane, k0, k1):
     """The product's random word for (stream, lane, period t): word t % 4 of the Philox block with
     counter (gid, ep, t // 4, stream << 16 | lane) (imenv_device.h rng_word)."""
     return philox4x32_10(gid, ep, int(t) >> 2, (int(stream) << 16) | int(lane), k0, k1)[int(t) & 3]
+
+
+def node_word(gid, ep, t, stream, node, k0, k1):
+    """Noisy-delay word for (node, period t): word node % 4 of the Philox block with counter
+    (gid, ep, t, stream << 16 | node // 4) (imenv_device.h rng_node_block)."""
+    return philox4x32_10(gid, ep, int(t), (int(stream) << 16) | (int(node) >> 2), k0, k1)[int(node) & 3]
 
 
 def split_seed(seed):
