@@ -31,8 +31,13 @@ def cc_observation(obs, actions=None, clip=(-1.0, 1.0), out=None):
         a = actions.to(device=obs.device).contiguous().reshape(B, N)
         if a.dtype not in (torch.float32, torch.float64):
             a = a.to(torch.float64)
+    W = N * F + N - 1
     if out is None:
-        out = torch.empty((B, N, N * F + N - 1), dtype=obs.dtype, device=obs.device)
+        out = torch.empty((B, N, W), dtype=obs.dtype, device=obs.device)
+    elif (out.dtype != obs.dtype or out.device != obs.device or not out.is_contiguous() or
+          out.numel() != B * N * W):
+        raise ValueError("out must be a contiguous %s tensor of %d x %d x %d values on %s"
+                         % (obs.dtype, B, N, W, obs.device))
     lib = nat.load()
     st = torch.cuda.current_stream(obs.device).cuda_stream
     nat.check(lib.imenv_cc_observation(B, N, F, o.data_ptr(), nat.F64 if o.dtype == torch.float64 else nat.F32,

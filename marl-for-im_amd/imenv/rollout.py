@@ -48,12 +48,13 @@ class RolloutBuffer:
         adv, vt = buf.advantages()
     """
 
-    def __init__(self, env, obs_dtype=torch.float32, reward_dtype=torch.float64):
+    def __init__(self, env, obs_dtype=torch.float32):
+        # rewards are float64, the dtype the env writes (the reference's profit arithmetic)
         T, n, N, F = env.T, env.n, env.N, env.F
         dev = env.device
         self.obs = torch.empty((T + 1, n, N, F), dtype=obs_dtype, device=dev)
         self.actions = torch.empty((T, n, N), dtype=torch.float32, device=dev)
-        self.rewards = torch.empty((T,) + tuple(env.reward_shape()), dtype=reward_dtype, device=dev)
+        self.rewards = torch.empty((T,) + tuple(env.reward_shape()), dtype=torch.float64, device=dev)
         self.values = torch.empty((T, n), dtype=torch.float32, device=dev)
 
     def advantages(self, gamma=0.99, lambda_=0.95, last_value=None):

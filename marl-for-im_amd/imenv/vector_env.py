@@ -63,6 +63,18 @@ class VectorInvEnv:
     def _obs_code(self, dtype):
         return nat.F64 if dtype == torch.float64 else nat.F32
 
+    def _out(self, t, shape, dtypes, what):
+        """A caller-owned output buffer the kernel writes in place: checked before any launch (a
+        wrong-sized buffer would be written out of bounds), else a fresh tensor."""
+        if t is None:
+            return torch.empty(shape, dtype=dtypes[0], device=self.device)
+        if not torch.is_tensor(t) or t.device != self.device or t.dtype not in dtypes or \
+                tuple(t.shape) != tuple(shape) or not t.is_contiguous():
+            raise ValueError("%s must be a contiguous %s tensor of shape %s on %s (got %s)" % (
+                what, "/".join(str(d) for d in dtypes), tuple(shape), self.device,
+                (tuple(t.shape), t.dtype, t.device, t.is_contiguous()) if torch.is_tensor(t) else type(t)))
+        return t
+
     def reward_shape(self):
         return (self.n, self.N) if self.spec.reward_mode == nat.REWARD_INDEPENDENT else (self.n,)
 
@@ -117,8 +129,7 @@ class VectorInvEnv:
             u = u.permute(1, 2, 0).contiguous()
             keep.append(u)
             uptr = u.data_ptr()
-        obs = obs_out if obs_out is not None else torch.empty(
-            (self.n, self.N, self.F), dtype=self.obs_dtype, device=self.device)
+        obs = self._out(obs_out, (self.n, self.N, self.F), (self.obs_dtype, torch.float32, torch.float64), "obs_out")
         ep = -1 if episode is None else int(episode)
         nat.check(self.lib.imenv_reset(self._h, dptr, layout, int(bool(noisy_delay)), float(noisy_delay_threshold),
                                        uptr, ep, obs.data_ptr(), self._obs_code(obs.dtype), self._stream()),
@@ -141,10 +152,8 @@ class VectorInvEnv:
         if a.device != self.device or a.dtype not in (torch.float32, torch.float64):
             a = a.to(device=self.device, dtype=torch.float64 if a.dtype == torch.float64 else torch.float32)
         a = a.reshape(self.n, self.N).contiguous()
-        obs = obs_out if obs_out is not None else torch.empty(
-            (self.n, self.N, self.F), dtype=self.obs_dtype, device=self.device)
-        rew = reward_out if reward_out is not None else torch.empty(
-            self.reward_shape(), dtype=torch.float64, device=self.device)
+        obs = self._out(obs_out, (self.n, self.N, self.F), (self.obs_dtype, torch.float32, torch.float64), "obs_out")
+        rew = self._out(reward_out, self.reward_shape(), (torch.float64,), "reward_out")
         inf = None
         iptr = None
         if info:

@@ -315,3 +315,22 @@ def test_gpu_step_traffic_matches_bench_formula():
     steady, _ = env.step_traffic()
     assert steady == 16 + 24 + 4 + 1 + 4 + 32 + 96 + 8
     env.close()
+
+
+def test_gpu_output_buffers_are_checked_before_launch():
+    """Caller-owned obs / reward buffers of the wrong shape, dtype or device raise before any kernel
+    writes into them (a short buffer would otherwise be written out of bounds)."""
+    env = _env("MAIM", C2, 256)
+    obs0 = torch.empty((256, 4, 3), dtype=torch.float32, device=DEV)
+    env.reset(obs_out=obs0)
+    a = torch.zeros((256, 4), device=DEV)
+    for bad in (torch.empty((255, 4, 3), device=DEV), torch.empty((256, 4, 3), dtype=torch.float16, device=DEV),
+                torch.empty((256, 4, 3)), torch.empty((256, 3, 4), device=DEV).transpose(1, 2)):
+        with pytest.raises(ValueError):
+            env.step(a, obs_out=bad)
+    with pytest.raises(ValueError):
+        env.step(a, reward_out=torch.empty(256, dtype=torch.float32, device=DEV))
+    with pytest.raises(ValueError):
+        env.reset(obs_out=torch.empty((128, 4, 3), device=DEV))
+    assert env.state()["period"] == 0        # nothing was launched by the rejected calls
+    env.close()

@@ -121,6 +121,51 @@ __global__ void __launch_bounds__(BS) probe_u8_ept2(const P3Args A) {
   }
 }
 
+// persistent blocks over 256-env tiles (tile += gridDim), the next tile's loads issued before the
+// current tile's arithmetic and stores (software pipelining: more bytes in flight per wave)
+struct P3Tile {
+  float4 a;
+  uint32_t vi, vb, vo;
+  uint8_t r[4];
+};
+__device__ __forceinline__ void p3_load(const P3Args& A, int64_t e, P3Tile& x) {
+  x.a = A.act[e];
+  x.vi = A.inv[e]; x.vb = A.bl[e]; x.vo = A.ou[e];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x.r[i] = A.ring[(int64_t)A.ring_row[i] * A.n + e];
+}
+template <int BS>
+__global__ void __launch_bounds__(BS) probe_u8_persist(const P3Args A) {
+  __shared__ __attribute__((aligned(16))) float s_obs[BS * 12];
+  const int tid = threadIdx.x;
+  const int64_t ntiles = A.n / BS;
+  int64_t tile = blockIdx.x;
+  P3Tile cur, nxt;
+  if (tile < ntiles) p3_load(A, tile * BS + tid, cur);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int64_t e = tile * BS + tid;
+    const int64_t tn = tile + gridDim.x;
+    if (tn < ntiles) p3_load(A, tn * BS + tid, nxt);
+    const uint32_t s = cur.vi + cur.vb + cur.vo + cur.r[0] + cur.r[1] + cur.r[2] + cur.r[3] + (uint32_t)cur.a.x;
+    A.inv[e] = cur.vi + s;
+    A.bl[e] = cur.vb ^ s;
+    A.ou[e] = cur.vo - s;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) A.ring[(int64_t)A.ring_row[i] * A.n + e] = (uint8_t)(cur.r[i] + s);
+    const float f = (float)s;
+#pragma unroll
+    for (int q = 0; q < 12; ++q) s_obs[tid * 12 + q] = f + (float)q * cur.a.y;
+    __syncthreads();
+    float4* g4 = reinterpret_cast<float4*>(A.obs + (tile * BS) * 12);
+    const float4* s4 = reinterpret_cast<const float4*>(s_obs);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) g4[q * BS + tid] = s4[q * BS + tid];
+    A.rew[e] = (double)s * cur.a.z;
+    __syncthreads();
+    cur = nxt;
+  }
+}
+
 extern "C" int probe3_run(int which, const P3Args* A, void* stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t n = A->n;
@@ -131,6 +176,9 @@ extern "C" int probe3_run(int which, const P3Args* A, void* stream) {
     case 3: hipLaunchKernelGGL((probe_u8x4<64>), dim3(n / 256), dim3(64), 0, st, *A); break;
     case 4: hipLaunchKernelGGL((probe_u8x4<128>), dim3(n / 512), dim3(128), 0, st, *A); break;
     case 5: hipLaunchKernelGGL((probe_u8x4<256>), dim3(n / 1024), dim3(256), 0, st, *A); break;
+    case 6: hipLaunchKernelGGL((probe_u8_persist<256>), dim3(2048), dim3(256), 0, st, *A); break;
+    case 7: hipLaunchKernelGGL((probe_u8_persist<256>), dim3(1024), dim3(256), 0, st, *A); break;
+    case 8: hipLaunchKernelGGL((probe_u8_persist<256>), dim3(512), dim3(256), 0, st, *A); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;

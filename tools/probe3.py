@@ -13,7 +13,8 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "marl-for-im_amd"))
 SRC = os.path.join(HERE, "probe3.hip")
 LIB = os.path.join(HERE, "_lib", "libprobe3.so")
-NAMES = ["u8_bs256", "u8_bs512", "u8_ept2", "u8x4_bs64", "u8x4_bs128", "u8x4_bs256"]
+NAMES = ["u8_bs256", "u8_bs512", "u8_ept2", "u8x4_bs64", "u8x4_bs128", "u8x4_bs256", "persist_g2048",
+         "persist_g1024", "persist_g512"]
 
 
 class P3Args(ctypes.Structure):
