@@ -24,6 +24,8 @@ import torch
 from . import _native as nat
 from .spec import HostSpec, build_spec
 
+_FLOATS = (torch.float32, torch.float64)
+
 
 class VectorInvEnv:
     def __init__(self, kind_or_spec, config=None, n_envs=1, device=None, env_offset=0,
@@ -55,9 +57,16 @@ class VectorInvEnv:
         self.period = 0
         self.episode = -1
         self._keep = []
+        self._done = c_int32(0)
+        self._done_ref = byref(self._done)
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
+        # the raw handle of the current stream (the public torch.cuda.current_stream() builds a Stream
+        # object per call: a few microseconds of the per-step host cost)
+        raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        if raw is not None:
+            return c_void_p(raw(self.device.index))
         return c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     def _obs_code(self, dtype):
@@ -69,7 +78,7 @@ class VectorInvEnv:
         if t is None:
             return torch.empty(shape, dtype=dtypes[0], device=self.device)
         if not torch.is_tensor(t) or t.device != self.device or t.dtype not in dtypes or \
-                tuple(t.shape) != tuple(shape) or not t.is_contiguous():
+                t.shape != shape or not t.is_contiguous():
             raise ValueError("%s must be a contiguous %s tensor of shape %s on %s (got %s)" % (
                 what, "/".join(str(d) for d in dtypes), tuple(shape), self.device,
                 (tuple(t.shape), t.dtype, t.device, t.is_contiguous()) if torch.is_tensor(t) else type(t)))
@@ -148,10 +157,14 @@ class VectorInvEnv:
 
     def step(self, actions, obs_out=None, reward_out=None, info=False):
         """step(action) (IM_env.py:287-360): actions [n, N] (or [n*N]) in the spec's action units."""
-        a = actions if torch.is_tensor(actions) else torch.as_tensor(np.asarray(actions))
-        if a.device != self.device or a.dtype not in (torch.float32, torch.float64):
-            a = a.to(device=self.device, dtype=torch.float64 if a.dtype == torch.float64 else torch.float32)
-        a = a.reshape(self.n, self.N).contiguous()
+        a = actions
+        # fast path: a contiguous float device tensor of n*N values is passed as is
+        if not (torch.is_tensor(a) and a.device == self.device and a.dtype in _FLOATS and a.is_contiguous() and
+                a.numel() == self.n * self.N):
+            a = a if torch.is_tensor(a) else torch.as_tensor(np.asarray(a))
+            if a.device != self.device or a.dtype not in _FLOATS:
+                a = a.to(device=self.device, dtype=torch.float64 if a.dtype == torch.float64 else torch.float32)
+            a = a.reshape(self.n, self.N).contiguous()
         obs = self._out(obs_out, (self.n, self.N, self.F), (self.obs_dtype, torch.float32, torch.float64), "obs_out")
         rew = self._out(reward_out, self.reward_shape(), (torch.float64,), "reward_out")
         inf = None
@@ -164,10 +177,12 @@ class VectorInvEnv:
             ci = nat.ImEnvInfo(*[inf[k].data_ptr() for k in ("order", "demand", "acquisition", "ship",
                                                                "profit", "ship_to", "backlog_to")])
             iptr = byref(ci)
-        done = c_int32(0)
-        nat.check(self.lib.imenv_step(self._h, a.data_ptr(), nat.F64 if a.dtype == torch.float64 else nat.F32,
-                                      obs.data_ptr(), self._obs_code(obs.dtype), rew.data_ptr(), iptr,
-                                      byref(done), self._stream()), "imenv_step")
+        done = self._done
+        rc = self.lib.imenv_step(self._h, a.data_ptr(), nat.F64 if a.dtype == torch.float64 else nat.F32,
+                                 obs.data_ptr(), nat.F64 if obs.dtype == torch.float64 else nat.F32, rew.data_ptr(),
+                                 iptr, self._done_ref, self._stream())
+        if rc:
+            nat.check(rc, "imenv_step")
         self._keep = [a]
         self.period += 1
         return obs, rew, bool(done.value), inf
