@@ -212,7 +212,13 @@ def main():
             if events is not None and t == 1 and s + T - 1 <= steps:
                 pair = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 pair[0].record(stream)
-            rc = lib.imenv_step(h, a_ptr[t], nat.F32, o_ptr[t], nat.F32, r_ptr[t], None, None, sptr)
+            if gather is None:
+                rc = lib.imenv_step(h, a_ptr[t], nat.F32, o_ptr[t], nat.F32, r_ptr[t], None, None, sptr)
+            else:
+                # the env writes straight into the packed send buffer of step s (double-buffered); the
+                # all-gather of step s runs on RCCL's stream under step s+1
+                rc = lib.imenv_step(h, a_ptr[t], nat.F32, gather.obs_out(s).data_ptr(), nat.F32,
+                                    gather.reward_out(s).data_ptr(), None, None, sptr)
             if rc:
                 nat.check(rc, "imenv_step")
             if pair is not None and t == T - 1:
@@ -220,7 +226,11 @@ def main():
                 events.append(pair)
                 pair = None
             if gather is not None:
-                gather(obs_buf[t], rew_buf[t])
+                gather.start(s)
+                if s >= 1:
+                    gather.result(s - 1)     # the learner's view of step s-1: [world*n, N, F], [world*n]
+        if gather is not None and steps:
+            gather.result(steps - 1)
 
     # warmup (whole episodes so the timed region starts at a reset)
     w = ((args.warmup + T - 1) // T) * T

@@ -3,11 +3,22 @@
 Envs are independent (no cross-env term anywhere in step()), so the data path
 has no collective: rank r steps envs [offset_r, offset_r + n_r) on its own GPU, and every
 random draw is keyed by the GLOBAL env id (Philox counter, imenv.h), so trajectories do not
-depend on the number of ranks. The only exchange is optional: gathering each step's observations
-and rewards to every rank (a centralised learner), one RCCL all-gather per step.
+depend on the number of ranks. The only exchange is optional: gathering observations and rewards
+to every rank (a centralised learner).
+
+The gather packs every field of one exchange into ONE byte buffer, so one RCCL all-gather moves
+them all. The env writes straight into that buffer (``obs_out`` / ``reward_out`` views), so there is
+no packing copy. xGMI links are point to point (7 links per GPU), so a ring all-gather is bound per
+link. Fewer, larger collectives therefore win:
+- ``StepGather``: one collective per step, double-buffered. The collective of step t overlaps step
+  t+1 on RCCL's stream (``async_op``); the send buffer is reused only after that collective completes.
+- ``EpisodeGather``: one collective per episode over the whole [T+1, n, ...] rollout. It moves 30x
+  the bytes per call and makes 30x fewer calls.
 """
 import torch
 import torch.distributed as dist
+
+_ALIGN = 256     # every field starts on a 256-byte boundary of the packed buffer
 
 
 def shard_range(total_envs, world_size, rank):
@@ -26,29 +37,120 @@ def weak_offset(n_per_rank, rank):
     return int(rank) * int(n_per_rank)
 
 
-class StepGather:
-    """All-gathers one step's obs [n, N, F] and reward [n] / [n, N] from every rank (equal n).
+class PackedGather:
+    """All-gather of several tensors (equal shapes on every rank) as one packed byte buffer.
 
-    Buffers are allocated once; NCCL (RCCL) uses all_gather_into_tensor straight into them, other
-    backends (gloo, CPU tests) all_gather a list and copy.
+    fields: [(shape, dtype), ...]. ``send(k)`` gives the fields of send buffer k as contiguous views
+    to write into (VectorInvEnv.step(obs_out=..., reward_out=...) accepts them). ``gathered(k)`` gives
+    every field of receive buffer k as a [world, *shape] view. ``start(k)`` launches the collective of
+    buffer k and ``wait(k)`` orders the current stream after it.
     """
 
-    def __init__(self, obs_like, reward_like, group=None):
+    def __init__(self, fields, device, group=None, buffers=1):
         self.group = group
         self.world = dist.get_world_size(group)
-        self.obs = torch.empty((self.world * obs_like.shape[0],) + tuple(obs_like.shape[1:]), dtype=obs_like.dtype,
-                               device=obs_like.device)
-        self.reward = torch.empty((self.world * reward_like.shape[0],) + tuple(reward_like.shape[1:]),
-                                  dtype=reward_like.dtype, device=reward_like.device)
+        self.fields = [(tuple(int(s) for s in shape), dtype) for shape, dtype in fields]
+        self.offsets, off = [], 0
+        for shape, dtype in self.fields:
+            self.offsets.append(off)
+            nbytes = torch.Size(shape).numel() * torch.empty((), dtype=dtype).element_size()
+            off += (nbytes + _ALIGN - 1) // _ALIGN * _ALIGN
+        self.chunk = off
+        self.device = torch.device(device)
+        self._send = [torch.empty(self.chunk, dtype=torch.uint8, device=self.device) for _ in range(buffers)]
+        self._recv = [torch.empty(self.world * self.chunk, dtype=torch.uint8, device=self.device)
+                      for _ in range(buffers)]
+        self._work = [None] * buffers
         self._into = dist.get_backend(group) == "nccl"
 
-    def _one(self, out, x):
+    def _field(self, buf, j, lead=()):
+        shape, dtype = self.fields[j]
+        nbytes = torch.Size(shape).numel() * torch.empty((), dtype=dtype).element_size()
+        o = self.offsets[j]
+        if not lead:
+            return buf[o:o + nbytes].view(dtype).view(shape)
+        rows = buf.view(self.world, self.chunk)[:, o:o + nbytes]     # [world, nbytes], rows contiguous
+        return rows.view(dtype).view((self.world,) + shape)
+
+    def send(self, k=0):
+        return [self._field(self._send[k], j) for j in range(len(self.fields))]
+
+    def gathered(self, k=0):
+        return [self._field(self._recv[k], j, lead=(self.world,)) for j in range(len(self.fields))]
+
+    def start(self, k=0):
+        """Launch the all-gather of send buffer k (async: RCCL's stream waits for the work already
+        queued on the current stream, the current stream does not wait for the collective)."""
+        self.wait(k)         # a previous collective on these buffers must be complete first
         if self._into:
-            dist.all_gather_into_tensor(out, x.contiguous(), group=self.group)
+            self._work[k] = dist.all_gather_into_tensor(self._recv[k], self._send[k], group=self.group,
+                                                        async_op=True)
         else:
-            dist.all_gather(list(out.chunk(self.world, dim=0)), x.contiguous(), group=self.group)   # views
+            self._work[k] = dist.all_gather(list(self._recv[k].chunk(self.world)), self._send[k], group=self.group,
+                                            async_op=True)
+
+    def wait(self, k=0):
+        w = self._work[k]
+        if w is not None:
+            w.wait()          # NCCL: a stream dependency, not a host block
+            self._work[k] = None
+
+    def __call__(self, *tensors, k=0):
+        """Copy tensors into send buffer k, gather synchronously, return the [world, ...] views."""
+        self.wait(k)
+        for dst, src in zip(self.send(k), tensors):
+            dst.copy_(src)
+        self.start(k)
+        self.wait(k)
+        return self.gathered(k)
+
+
+class StepGather(PackedGather):
+    """One step's obs [n, N, F] and reward [n] / [n, N] from every rank, double-buffered: the env of
+    step t writes into ``obs_out(t)`` / ``reward_out(t)`` (buffer t % 2), ``start(t)`` launches the
+    gather, which overlaps step t+1; ``result(t)`` waits for it and returns (obs [world*n, N, F],
+    reward [world*n, ...]) views."""
+
+    def __init__(self, obs_like, reward_like, group=None, buffers=2):
+        super().__init__([(obs_like.shape, obs_like.dtype), (reward_like.shape, reward_like.dtype)],
+                         obs_like.device, group, buffers)
+        self.nbuf = buffers
+
+    def obs_out(self, t):
+        """Send view for step t's obs. Orders the current stream after the collective that last read
+        this buffer (step t - nbuf), so the env cannot overwrite it while it is in flight."""
+        self.wait(t % self.nbuf)
+        return self.send(t % self.nbuf)[0]
+
+    def reward_out(self, t):
+        self.wait(t % self.nbuf)
+        return self.send(t % self.nbuf)[1]
+
+    def start(self, t=0):
+        super().start(t % self.nbuf)
+
+    def result(self, t):
+        self.wait(t % self.nbuf)
+        o, r = self.gathered(t % self.nbuf)
+        return o.flatten(0, 1), r.flatten(0, 1)
 
     def __call__(self, obs, reward):
-        self._one(self.obs, obs)
-        self._one(self.reward, reward)
-        return self.obs, self.reward
+        """Compatibility: copy one step's obs / reward in and gather synchronously (buffer 0)."""
+        o, r = PackedGather.__call__(self, obs, reward, k=0)
+        return o.flatten(0, 1), r.flatten(0, 1)
+
+
+class EpisodeGather(PackedGather):
+    """A whole episode's rollout (obs [T+1, n, N, F], rewards [T, n(, N)]) in one collective: the env
+    writes every period into ``obs`` / ``rewards`` (views of the send buffer); ``start()`` after the
+    last step; ``result()`` -> [world, T+1, n, N, F] and [world, T, n(, N)] views."""
+
+    def __init__(self, env, group=None, obs_dtype=torch.float32):
+        T, n, N, F = env.T, env.n, env.N, env.F
+        super().__init__([((T + 1, n, N, F), obs_dtype), ((T,) + tuple(env.reward_shape()), torch.float64)],
+                         env.device, group, 1)
+        self.obs, self.rewards = self.send(0)
+
+    def result(self):
+        self.wait(0)
+        return self.gathered(0)

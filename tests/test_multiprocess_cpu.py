@@ -103,3 +103,59 @@ def test_shard_range_partitions_ids():
                 assert o1 + c1 == o2
             assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
     assert weak_offset(1 << 20, 3) == 3 << 20
+
+
+class _EnvShape:
+    """The attributes EpisodeGather reads from a VectorInvEnv (CPU stand-in for the gloo test)."""
+    def __init__(self, T, n, N, F, independent):
+        self.T, self.n, self.N, self.F = T, n, N, F
+        self.device = torch.device("cpu")
+        self._ind = independent
+
+    def reward_shape(self):
+        return (self.n, self.N) if self._ind else (self.n,)
+
+
+def _packed_worker(rank, world, port, out_path):
+    from imenv.shard import EpisodeGather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, N, F, T = 5, 4, 3, 30
+        # per-step, double-buffered: write step t into buffer t % 2 while step t-1's gather is in flight
+        g = StepGather(torch.zeros((n, N, F)), torch.zeros(n, dtype=torch.float64))
+        steps = []
+        for t in range(6):
+            g.obs_out(t).copy_(torch.full((n, N, F), 100.0 * rank + t))
+            g.reward_out(t).copy_(torch.arange(n, dtype=torch.float64) + 1000 * rank + t)
+            g.start(t)
+            if t >= 1:
+                steps.append([x.clone() for x in g.result(t - 1)])
+        steps.append([x.clone() for x in g.result(5)])
+        # per-episode: one collective over the whole rollout, independent (per-agent) rewards
+        eg = EpisodeGather(_EnvShape(T, n, N, F, independent=True))
+        eg.obs.copy_(torch.arange((T + 1) * n * N * F, dtype=torch.float32).view(T + 1, n, N, F) + rank)
+        eg.rewards.copy_(torch.full((T, n, N), -1.0 - rank, dtype=torch.float64))
+        eg.start()
+        eo, er = eg.result()
+        if rank == 0:
+            torch.save(dict(steps=steps, eo=eo.clone(), er=er.clone()), out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_packed_step_and_episode_gathers(tmp_path):
+    out = str(tmp_path / "packed.pt")
+    mp.spawn(_packed_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    n, N, F, T = 5, 4, 3, 30
+    for t, (o, r) in enumerate(got["steps"]):
+        assert o.shape == (2 * n, N, F) and r.shape == (2 * n,)
+        for rank in range(2):
+            assert torch.equal(o[rank * n:(rank + 1) * n], torch.full((n, N, F), 100.0 * rank + t))
+            assert torch.equal(r[rank * n:(rank + 1) * n], torch.arange(n, dtype=torch.float64) + 1000 * rank + t)
+    base = torch.arange((T + 1) * n * N * F, dtype=torch.float32).view(T + 1, n, N, F)
+    assert got["eo"].shape == (2, T + 1, n, N, F) and got["er"].shape == (2, T, n, N)
+    for rank in range(2):
+        assert torch.equal(got["eo"][rank], base + rank)
+        assert torch.equal(got["er"][rank], torch.full((T, n, N), -1.0 - rank, dtype=torch.float64))
