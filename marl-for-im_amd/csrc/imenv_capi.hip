@@ -56,13 +56,17 @@ __global__ void __launch_bounds__(256) imenv_reset_kernel(const SpecDev* __restr
   }
 }
 
-// packed [n][np] state rows -> int32 [N][n] SoA (imenv_get_state)
+// packed [n][np] state rows -> int32 [N][n] SoA (imenv_get_state). part: 0 the value itself, 1 its
+// positive part (inventory from the net row), 2 its negative part (backlog from the net row)
 template <typename ST>
 __global__ void __launch_bounds__(256) imenv_unpack_kernel(const ST* __restrict__ src, int32_t* __restrict__ dst,
-                                                           int64_t n, int np, int N) {
+                                                           int64_t n, int np, int N, int part) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
-  for (int i = 0; i < N; ++i) dst[i * n + e] = (int32_t)src[e * np + i];
+  for (int i = 0; i < N; ++i) {
+    const int32_t v = (int32_t)src[e * np + i];
+    dst[i * n + e] = part == 0 ? v : (part == 1 ? max(v, 0) : max(-v, 0));
+  }
 }
 
 // policy_stats of a base-stock rollout: one block per (policy, metric) merges the rollout kernel's
@@ -329,6 +333,18 @@ int64_t state_bound(const ImEnvSpec& s) {
   return B;
 }
 
+// Largest magnitude of the signed net-inventory row (inv - backlog): inventory up to its capacity or
+// initial level, backlog up to its cap or T periods of demand.
+int64_t net_bound(const ImEnvSpec& s) {
+  int64_t B = 0;
+  for (int i = 0; i < s.num_nodes; ++i) {
+    const int64_t dm = demand_bound(s, i);
+    const int64_t blb = s.backlog_cap[i] >= 0 ? s.backlog_cap[i] : (int64_t)s.num_periods * dm;
+    B = std::max<int64_t>(B, std::max<int64_t>(blb, std::max<int64_t>(s.inv_max[i], s.init_inv[i])));
+  }
+  return B;
+}
+
 int validate_and_derive(const ImEnvSpec& s, SpecDev& d, int& maxc) {
   if (s.abi_version != IMENV_ABI_VERSION) return fail(IMENV_E_INVALID, "abi_version mismatch");
   const int N = s.num_nodes;
@@ -430,6 +446,7 @@ int validate_and_derive(const ImEnvSpec& s, SpecDev& d, int& maxc) {
   // narrowest element type the bounds allow; IMENV_STATE_BYTES=2|4 forces a wider one (testing)
   const int64_t bound = state_bound(s);
   d.es = bound <= 255 ? 1 : (bound <= 32767 ? 2 : 4);
+  if (d.es == 1 && net_bound(s) > 127) d.es = 2;   // the net row is signed (int8 beside uint8 rows)
   if (const char* v = std::getenv("IMENV_STATE_BYTES")) {
     const int want = std::atoi(v);
     if ((want == 2 || want == 4) && want > d.es) d.es = want;
@@ -463,7 +480,7 @@ struct ImEnv {
   int64_t env_offset = 0;
   int maxc = 0;
   size_t es = 4;       // state element size (1, 2 or 4)
-  void *d_inv = nullptr, *d_bl = nullptr, *d_ou = nullptr, *d_ring = nullptr, *d_hist_d = nullptr, *d_hist_o = nullptr;
+  void *d_net = nullptr, *d_ou = nullptr, *d_ring = nullptr, *d_hist_d = nullptr, *d_hist_o = nullptr;
   int32_t *d_carry = nullptr, *d_bto = nullptr, *d_demand = nullptr;
   double* d_delay_u = nullptr;
   float* d_lut32 = nullptr;
@@ -505,7 +522,7 @@ const char* imenv_last_error(void) { return g_err.c_str(); }
 void imenv_destroy(ImEnv* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
-  void* ptrs[] = {h->d_spec, h->d_inv, h->d_bl, h->d_ou, h->d_ring, h->d_carry, h->d_bto, h->d_hist_d,
+  void* ptrs[] = {h->d_spec, h->d_net, h->d_ou, h->d_ring, h->d_carry, h->d_bto, h->d_hist_d,
                   h->d_hist_o, h->d_demand, h->d_delay_u, h->d_err, h->d_err_any, h->d_lut32, h->d_lut64,
                   h->d_episode, h->d_roll_part};
   for (void* p : ptrs)
@@ -540,9 +557,9 @@ int imenv_create(const ImEnvSpec* spec, int64_t n_envs, int64_t env_offset, int 
       uses_hist = true;
   hipError_t he = hipSetDevice(device);
   if (he != hipSuccess) { delete h; return fail(IMENV_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(he)); }
-  char **inv = reinterpret_cast<char**>(&h->d_inv), **bl = reinterpret_cast<char**>(&h->d_bl),
-       **ou = reinterpret_cast<char**>(&h->d_ou), **ring = reinterpret_cast<char**>(&h->d_ring);
-  if ((rc = alloc(&h->d_spec, 1)) || (rc = alloc(inv, rowb)) || (rc = alloc(bl, rowb)) || (rc = alloc(ou, rowb)) ||
+  char **net = reinterpret_cast<char**>(&h->d_net), **ou = reinterpret_cast<char**>(&h->d_ou),
+       **ring = reinterpret_cast<char**>(&h->d_ring);
+  if ((rc = alloc(&h->d_spec, 1)) || (rc = alloc(net, rowb)) || (rc = alloc(ou, rowb)) ||
       (rc = alloc(ring, n * h->es * h->host.ring_total)) || (rc = alloc(&h->d_carry, n * np)) ||
       (rc = alloc(&h->d_bto, h->maxc > 0 ? n * np : 0)) || (rc = alloc(&h->d_err, n)) ||
       (rc = alloc(&h->d_err_any, 1)) || (rc = alloc(&h->d_episode, 1))) {
@@ -643,7 +660,7 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
   A.actions = actions;
   A.obs = obs;
   A.reward = reward;
-  A.inv = h->d_inv; A.bl = h->d_bl; A.ou = h->d_ou;
+  A.net = h->d_net; A.ou = h->d_ou;
   A.ring = h->d_ring; A.carry = h->d_carry; A.bto = h->d_bto;
   A.hist_d = h->d_hist_d; A.hist_o = h->d_hist_o;
   A.demand = h->d_demand;
@@ -905,19 +922,24 @@ int imenv_get_state(ImEnv* h, int32_t* inv, int32_t* backlog, int32_t* order_u, 
     if (order_u) HIPCHK(hipMemsetAsync(order_u, 0, bytes, st));
   } else {
     const unsigned grid = (unsigned)((h->n + 255) / 256);
-    void* src[3] = {h->d_inv, h->d_bl, h->d_ou};
+    // inventory and backlog are the two sides of the signed net row (imenv_device.h, NetOf)
+    void* src[3] = {h->d_net, h->d_net, h->d_ou};
     int32_t* dst[3] = {inv, backlog, order_u};
     for (int k = 0; k < 3; ++k) {
       if (!dst[k]) continue;
-      if (h->host.es == 1)
+      const int part = k == 0 ? 1 : (k == 1 ? 2 : 0);
+      if (h->host.es == 1 && k < 2)
+        hipLaunchKernelGGL(imenv_unpack_kernel<int8_t>, dim3(grid), dim3(256), 0, st,
+                           static_cast<const int8_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes, part);
+      else if (h->host.es == 1)
         hipLaunchKernelGGL(imenv_unpack_kernel<uint8_t>, dim3(grid), dim3(256), 0, st,
-                           static_cast<const uint8_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes);
+                           static_cast<const uint8_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes, part);
       else if (h->host.es == 2)
         hipLaunchKernelGGL(imenv_unpack_kernel<int16_t>, dim3(grid), dim3(256), 0, st,
-                           static_cast<const int16_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes);
+                           static_cast<const int16_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes, part);
       else
         hipLaunchKernelGGL(imenv_unpack_kernel<int32_t>, dim3(grid), dim3(256), 0, st,
-                           static_cast<const int32_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes);
+                           static_cast<const int32_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes, part);
     }
     HIPCHK(hipGetLastError());
   }

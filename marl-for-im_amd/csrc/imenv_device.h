@@ -15,7 +15,8 @@
 // HBM layout. ST = uint8 / int16 when the spec's bounds prove every value fits
 // (0..255 / 32767), else int32. NP = row length in ST elements (N rounded up so rows are 4-byte
 // aligned: to a multiple of 4 for uint8, of 2 for int16).
-//   inv, backlog, order_u   [n][NP] ST      one packed row per env: 8 B per lane for N=4 int16
+//   net, order_u            [n][NP] ST      one packed row per env: 4 B per lane for N=4 uint8; the
+//                                           net row holds inv - backlog (signed: NetOf<ST>)
 //   ring (in transit)       [sum d_i][n] ST node-major, d_i slots per node: node i's slot
 //                                           (t mod d_i) holds what arrives at t (shipped at t - d_i)
 //                                           and is then overwritten by what ships at t, so the
@@ -82,8 +83,7 @@ struct StepArgs {
   const void* actions;
   void* obs;
   double* reward;
-  void* inv;
-  void* bl;
+  void* net;                  // net inventory rows: inv - backlog (NetOf<ST>; see Row below)
   void* ou;
   void* ring;
   int32_t* carry;
@@ -321,7 +321,7 @@ struct Row {
   __device__ static __forceinline__ void unpack(const uint32_t (&w)[WORDS], int (&v)[NT]) {
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
-      if constexpr (ES == 1) v[i] = (int)((w[i >> 2] >> ((i & 3) * 8)) & 0xFFu);   // values are >= 0
+      if constexpr (ES == 1) v[i] = (int)(ST)(uint8_t)((w[i >> 2] >> ((i & 3) * 8)) & 0xFFu);   // sign per ST
       else if constexpr (ES == 2) v[i] = (int)(int16_t)((w[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu);
       else v[i] = (int)w[i];
     }
@@ -353,6 +353,15 @@ struct Row {
     }
   }
 };
+
+// Inventory and backlog share one signed row: net = inv - backlog. After every step one of the two is
+// zero (ship = min(backlog + demand, inv + acquisition): either the backlog is cleared or the
+// inventory is used up, IM_env.py:315-340), and period 0 has no backlog, so
+// inv = max(net, 0), backlog = max(-net, 0). One row read and written per step instead of two.
+// The row's element is the signed twin of the state type (validate_and_derive widens the state type
+// when a bound does not fit it).
+template <typename ST> struct NetOf { using type = ST; };
+template <> struct NetOf<uint8_t> { using type = int8_t; };
 
 // ---------------------------------------------------------------- runtime spec policy
 // Every accessor reads the spec from device memory (scalar loads). Per-call flags come from A.
@@ -694,7 +703,7 @@ struct StepLoad {
   using R = Row<typename P::ST, P::NT, P::EXACT>;
   using R32 = Row<int32_t, P::NT, P::EXACT>;
   uint32_t aw[2 * P::NT];
-  uint32_t w_inv[R::WORDS], w_bl[R::WORDS], w_ou[R::WORDS], w_cin[R32::WORDS], w_bto[R32::WORDS];
+  uint32_t w_net[R::WORDS], w_ou[R::WORDS], w_cin[R32::WORDS], w_bto[R32::WORDS];
   typename P::ST r_arr[P::NT];
   int cdem[P::NT];
   double du[P::NT];
@@ -710,21 +719,21 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
   using ST = typename P::ST;
   using R = Row<ST, NT, EXACT>;
   using R32 = Row<int32_t, NT, EXACT>;
+  using SN = typename NetOf<ST>::type;
+  using RN = Row<SN, NT, EXACT>;
   const int64_t n = A.n;
   const bool valid = e < n;
   const int N = p.N();
   const int np = p.np();
   const int t = A.t;
-  const ST* __restrict__ p_inv = static_cast<const ST*>(A.inv);
-  const ST* __restrict__ p_bl = static_cast<const ST*>(A.bl);
+  const SN* __restrict__ p_net = static_cast<const SN*>(A.net);
   const ST* __restrict__ p_ou = static_cast<const ST*>(A.ou);
   const ST* __restrict__ p_ring = static_cast<const ST*>(A.ring);
   const int32_t* __restrict__ p_carry = A.carry;
   const int32_t* __restrict__ p_bto = A.bto;
   // ================= (A) loads: raw words only, every independent load issued before any use
   uint32_t (&aw)[2 * NT] = L.aw;
-  uint32_t (&w_inv)[R::WORDS] = L.w_inv;
-  uint32_t (&w_bl)[R::WORDS] = L.w_bl;
+  uint32_t (&w_net)[R::WORDS] = L.w_net;
   uint32_t (&w_ou)[R::WORDS] = L.w_ou;
   uint32_t (&w_cin)[R32::WORDS] = L.w_cin;
   uint32_t (&w_bto)[R32::WORDS] = L.w_bto;
@@ -737,7 +746,7 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
 #pragma unroll
   for (int q = 0; q < 2 * NT; ++q) aw[q] = 0;
 #pragma unroll
-  for (int q = 0; q < R::WORDS; ++q) w_inv[q] = w_bl[q] = w_ou[q] = 0;
+  for (int q = 0; q < R::WORDS; ++q) w_net[q] = w_ou[q] = 0;
 #pragma unroll
   for (int q = 0; q < R32::WORDS; ++q) w_cin[q] = w_bto[q] = 0;
 #pragma unroll
@@ -767,8 +776,7 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
       }
     }
     // state and arrivals are loaded even at t == 0 (then ignored): unconditional, branch-free loads
-    R::load(p_inv, el, np, N, w_inv);
-    R::load(p_bl, el, np, N, w_bl);
+    RN::load(p_net, el, np, N, w_net);
     R::load(p_ou, el, np, N, w_ou);
 #pragma unroll
     for (int i = 0; i < NT; ++i)
@@ -824,6 +832,8 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   using ST = typename P::ST;
   using R = Row<ST, NT, EXACT>;
   using R32 = Row<int32_t, NT, EXACT>;
+  using SN = typename NetOf<ST>::type;
+  using RN = Row<SN, NT, EXACT>;
   const int tid = threadIdx.x;
   const int64_t n = A.n;
   const bool valid = e < n;
@@ -836,16 +846,14 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   const uint64_t seed = p.seed();
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 
-  ST* __restrict__ p_inv = static_cast<ST*>(A.inv);
-  ST* __restrict__ p_bl = static_cast<ST*>(A.bl);
+  SN* __restrict__ p_net = static_cast<SN*>(A.net);
   ST* __restrict__ p_ou = static_cast<ST*>(A.ou);
   ST* __restrict__ p_ring = static_cast<ST*>(A.ring);
   int32_t* __restrict__ p_carry = A.carry;
   int32_t* __restrict__ p_bto = A.bto;
   const int64_t ring_rows = n * np;   // elements per packed-row array (history)
   const uint32_t (&aw)[2 * NT] = L.aw;
-  const uint32_t (&w_inv)[R::WORDS] = L.w_inv;
-  const uint32_t (&w_bl)[R::WORDS] = L.w_bl;
+  const uint32_t (&w_net)[R::WORDS] = L.w_net;
   const uint32_t (&w_ou)[R::WORDS] = L.w_ou;
   const uint32_t (&w_cin)[R32::WORDS] = L.w_cin;
   const uint32_t (&w_bto)[R32::WORDS] = L.w_bto;
@@ -903,8 +911,12 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
     if (p.act_f64()) x[i] = __hiloint2double((int)aw[2 * i + 1], (int)aw[2 * i]);
     else x[i] = (double)__uint_as_float(aw[i]);
   }
-  R::unpack(w_inv, inv);
-  R::unpack(w_bl, bl);
+  RN::unpack(w_net, inv);
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {   // net -> (inv, backlog): one of them is 0
+    bl[i] = max(-inv[i], 0);
+    inv[i] = max(inv[i], 0);
+  }
   R::unpack(w_ou, ou);
 #pragma unroll
   for (int i = 0; i < NT; ++i) arr[i] = (int)r_arr[i];
@@ -955,8 +967,10 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
 
   // ================= (C) stores
   if (valid) {
-    R::store(p_inv, e, np, N, inv);
-    R::store(p_bl, e, np, N, bl);
+    int net[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) net[i] = inv[i] - bl[i];   // inv[i] * bl[i] == 0 after step_core
+    RN::store(p_net, e, np, N, net);
     R::store(p_ou, e, np, N, ou);
 #pragma unroll
     for (int i = 0; i < NT; ++i)

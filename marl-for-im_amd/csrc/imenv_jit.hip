@@ -308,6 +308,13 @@ std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f)
 
 namespace {
 std::mutex g_mu;
+
+// FNV-1a over the embedded device header (imenv_device.h): identifies the kernel body in tags
+unsigned device_src_hash() {
+  uint32_t h = 2166136261u;
+  for (const char* c = kRtcDeviceH; *c; ++c) h = (h ^ (uint8_t)*c) * 16777619u;
+  return h;
+}
 std::unordered_map<std::string, std::shared_ptr<const std::vector<char>>> g_code;
 
 std::vector<std::string> jit_options(const std::string& arch) {
@@ -404,8 +411,9 @@ bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const st
   out.bs = jit_step_block_size(d, base, f.obs_f64 ? 8 : 4);
   out.ept = jit_envs_per_thread(d, base, f.obs_f64);
   char tag[160];
-  std::snprintf(tag, sizeof tag, "jit:imenv_step_jit[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,ept=%d,%zuB]",
-                d.s.num_nodes, maxc, base ? 1 : 0, d.es, f.key(), out.bs, out.ept, src.size());
+  // dev=: hash of the device-code header, so a profile of an older kernel body never matches this one
+  std::snprintf(tag, sizeof tag, "jit:imenv_step_jit[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,ept=%d,%zuB,dev=%08x]",
+                d.s.num_nodes, maxc, base ? 1 : 0, d.es, f.key(), out.bs, out.ept, src.size(), device_src_hash());
   out.tag = tag;
   return true;
 }
@@ -469,8 +477,8 @@ bool jit_rollout_load(const SpecDev& d, int maxc, const RolloutFlags& f, const s
   if (!load_module(src, arch, "imenv_rollout_jit", out, msg)) return false;
   out.bs = bs;
   char tag[160];
-  std::snprintf(tag, sizeof tag, "jit:imenv_rollout_jit[N=%d,MC=%d,es=%d,flags=0x%x,bs=%d,%zuB]", d.s.num_nodes,
-                maxc, d.es, f.key(), bs, src.size());
+  std::snprintf(tag, sizeof tag, "jit:imenv_rollout_jit[N=%d,MC=%d,es=%d,flags=0x%x,bs=%d,%zuB,dev=%08x]",
+                d.s.num_nodes, maxc, d.es, f.key(), bs, src.size(), device_src_hash());
   out.tag = tag;
   return true;
 }

@@ -249,8 +249,9 @@ class VectorInvEnv:
     def step_traffic(self, action_bytes=4, obs_bytes=4, host_demand=False, metrics=False):
         """Algorithmic HBM bytes of one step() per env: (steady state, average over an episode).
 
-        The minimal traffic of this handle's layout: actions; inv / backlog / order_u
-        rows read + written (no read at t = 0: the initial state is implicit); node i's arrival read
+        The minimal traffic of this handle's layout: actions; the net-inventory
+        (inv - backlog) and order_u rows read + written (no read at t = 0: the initial state is
+        implicit); node i's arrival read
         (only once t >= d_i) and departure written; the time-dependent observation's other in-transit
         slots; int32 noisy-delay carry and divergent backlog_to rows; the demand / order history rows
         (written every step, read for the features j >= 1); the observation; the reward; optional
@@ -264,7 +265,7 @@ class VectorInvEnv:
         hist = any(g in (nat.G_DEMAND_HIST, nat.G_ORDER_HIST) and j >= 1 for g, j in s.features)
         per = []
         for t in range(T):
-            b = N * action_bytes + 3 * NP * es + (3 * NP * es if t > 0 else 0)
+            b = N * action_bytes + 2 * NP * es + (2 * NP * es if t > 0 else 0)
             b += es * sum(1 for i in range(N) if t >= d[i]) + N * es
             for rows in (s.noisy_delay, split):
                 if rows:

@@ -304,16 +304,17 @@ def test_gpu_ragged_env_counts(kind, cfg, odt):
 
 
 def test_gpu_step_traffic_matches_bench_formula():
-    """Algorithmic bytes per env-step for the bench layouts: C2 104 B steady,
-    103.367 B averaged over the 30-period episode."""
+    """Algorithmic bytes per env-step for the bench layouts: C2 96 B steady,
+    95.5 B averaged over the 30-period episode (t = 0 reads no state rows, node i no arrival
+    before t = d_i)."""
     env = _env("MAIM", C2, 64)
     assert env.state_layout()[0] == 1
     steady, avg = env.step_traffic()
-    assert steady == 104 and abs(avg - (104 - 19 / 30)) < 1e-9
+    assert steady == 96 and abs(avg - (96 - 15 / 30)) < 1e-9
     env.close()
     env = _env("MAIM_div", C4, 64)     # td slot of node 1 (delay 2), backlog_to rows, no history rows
     steady, _ = env.step_traffic()
-    assert steady == 16 + 24 + 4 + 1 + 4 + 32 + 96 + 8
+    assert steady == 16 + 16 + 4 + 1 + 4 + 32 + 96 + 8
     env.close()
 
 

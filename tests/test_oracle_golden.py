@@ -64,6 +64,24 @@ def test_oracle_matches_reference(name):
     np.testing.assert_array_equal(out["reward"], ref_r, err_msg=name)
 
 
+@pytest.mark.parametrize("name", CASES)
+def test_net_inventory_invariant(name):
+    """The kernel keeps one signed row net = inv - backlog: valid because after every
+    step of the reference either the inventory or the backlog is zero, on every golden trajectory
+    (and in the oracle over fresh random episodes with in-kernel-style draws)."""
+    meta, d = load_case(name)
+    assert d["inv"].min() >= 0 and d["backlog"].min() >= 0
+    assert not np.any(d["inv"] * d["backlog"]), name
+    env = OracleEnv(meta["kind"], meta["config"], n_envs=64)
+    rs = np.random.RandomState(5)
+    for ep in range(3):
+        env.reset(rng=dict(seed=7, episode=ep, env_offset=0, dist="poisson", mu=5))
+        for t in range(env.num_periods):
+            env.step(rs.uniform(-1.2, 1.2, size=(64, env.N)))
+            st = env.state_arrays()
+            assert not np.any(st["inv"] * st["backlog"]), (name, ep, t)
+
+
 def test_kats():
     k = load_kat()
     assert k["KAT0_demand"] == [2, 3, 11, 4, 8, 4, 3, 5, 9, 9, 5, 5, 8, 8, 6, 3, 4, 7, 3, 5, 3, 4, 7, 4,
