@@ -507,6 +507,8 @@ struct ImEnv {
   std::unordered_map<uint32_t, imenv::JitKernel> roll_k;
   double* d_roll_part = nullptr;
   size_t roll_part_cap = 0;
+  double* d_roll_terms = nullptr;   // parked objective terms of the single-pass tree rollout
+  size_t roll_terms_cap = 0;
   std::string last_rollout;
   double* d_metrics = nullptr;   // caller-owned [n][4 + N] (imenv_set_episode_metrics)
 };
@@ -524,7 +526,7 @@ void imenv_destroy(ImEnv* h) {
   (void)hipSetDevice(h->device);
   void* ptrs[] = {h->d_spec, h->d_net, h->d_ou, h->d_ring, h->d_carry, h->d_bto, h->d_hist_d,
                   h->d_hist_o, h->d_demand, h->d_delay_u, h->d_err, h->d_err_any, h->d_lut32, h->d_lut64,
-                  h->d_episode, h->d_roll_part};
+                  h->d_episode, h->d_roll_part, h->d_roll_terms};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& kv : h->jit_k)
@@ -799,8 +801,16 @@ int imenv_base_stock_rollout(ImEnv* h, const ImEnvRollout* r, void* stream) {
     if (rc) return rc;
     h->roll_part_cap = pneed;
   }
+  const size_t tneed = (size_t)imenv::rollout_term_slots(h->host, f) * P * bpp * k.bs;
+  if (h->roll_terms_cap < tneed) {
+    if (h->d_roll_terms) { HIPCHK(hipStreamSynchronize(st)); HIPCHK(hipFree(h->d_roll_terms)); h->d_roll_terms = nullptr; }
+    int rc = alloc(&h->d_roll_terms, tneed);
+    if (rc) return rc;
+    h->roll_terms_cap = tneed;
+  }
   imenv::RolloutArgs A;
   std::memset(&A, 0, sizeof(A));
+  A.terms = h->d_roll_terms;
   A.policy = r->policy;
   A.demand = r->demand;
   A.pmf = r->demand_pmf;

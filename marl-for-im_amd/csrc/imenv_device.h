@@ -127,6 +127,7 @@ struct RolloutArgs {
   const double* pmf;          // [pmf_len] dfo_func weight of a customer-demand value (objective only)
   double* ep;                 // [IMENV_NUM_STATS][P][S] per-episode metrics, or null
   double* partial;            // [IMENV_NUM_STATS][P][bpp][3] per-block (sum, M2, count)
+  double* terms;              // [P * bpp][TBUF][BS] parked objective terms (trees, rollout_body TBUF > 0)
   int64_t S;                  // scenarios per policy
   int64_t P;                  // policies
   int64_t bpp;                // blocks per policy = ceil(S / BS)
@@ -1284,7 +1285,11 @@ __device__ __forceinline__ double block_sum(double v, double* s_red) {
   return r;
 }
 
-template <class P, bool OBJ>
+// TBUF (trees, R > 1 retailers): 0 replays the episode once per retailer row (above); > 0 runs it once
+// and parks the terms of rows 1..R-1 in A.terms as [block][(r - 1) * T + t][thread] (TBUF = (R - 1) * T
+// doubles per thread: each block's scratch is one contiguous run, each wave store 512 contiguous
+// bytes), then adds them in index order after row 0's: the same np.sum order, one pass.
+template <class P, bool OBJ, int TBUF = 0>
 __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, const SpecDev* __restrict__ sp,
                                              uint32_t* s_thr, uint16_t* s_guide, int32_t* s_ring, double* s_pmf,
                                              int pmf_lds, double* s_red) {
@@ -1330,7 +1335,21 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
   for (int j = 0; j < 7; ++j) tail[j] = 0.0;
   int64_t inv_s = 0, bl_s = 0, cbl_s = 0;
 
-  const int passes = OBJ ? R : 1;
+  const int passes = (OBJ && TBUF == 0) ? R : 1;
+  double* __restrict__ my_terms = TBUF > 0 ? A.terms + (int64_t)blockIdx.x * (TBUF * BS) + tid : nullptr;
+  // one term into np.sum's pairwise accumulators: 8 interleaved partial sums over the first `full`
+  // indices, the rest kept for the sequential tail (NumPy's non-recursive block, n < 128)
+  auto add_term = [&](const int idx, const double term) {
+    if (idx < full) {
+      const int j = idx & 7;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc8[q] = (q == j) ? acc8[q] + term : acc8[q];
+    } else {
+      const int j = idx - full;
+#pragma unroll
+      for (int q = 0; q < 7; ++q) tail[q] = (q == j) ? term : tail[q];
+    }
+  };
 #pragma unroll 1
   for (int pass = 0; pass < passes; ++pass) {
     int inv[NT], bl[NT], ou[NT], btoc[NT], cin[NT];
@@ -1440,24 +1459,21 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
           const int r = (i < N) ? p.retailer_slot(i) : -1;
-          if (r == pass) {
+          if (TBUF > 0 ? r >= 0 : r == pass) {
             const int k = cust[i];
             const double w = (k >= 0 && k < pmf_n) ? s_pmf[k] : ((k >= pmf_n && k < A.pmf_len) ? A.pmf[k] : 0.0);
             const double term = w * rew;
-            const int idx = r * T + t;   // row-major [R][T]: this pass's terms arrive in index order
-            if (idx < full) {
-              const int j = idx & 7;
-#pragma unroll
-              for (int q = 0; q < 8; ++q) acc8[q] = (q == j) ? acc8[q] + term : acc8[q];
-            } else {
-              const int j = idx - full;
-#pragma unroll
-              for (int q = 0; q < 7; ++q) tail[q] = (q == j) ? term : tail[q];
-            }
+            if (TBUF > 0 && r > 0) my_terms[((r - 1) * T + t) * BS] = term;   // added after row 0
+            else add_term(r * T + t, term);   // row-major [R][T]: this pass's terms arrive in index order
           }
         }
       }
     }
+  }
+
+  if constexpr (OBJ && TBUF > 0) {
+#pragma unroll 1
+    for (int idx = T; idx < n_terms; ++idx) add_term(idx, my_terms[(idx - T) * BS]);
   }
 
   double obj = 0.0;

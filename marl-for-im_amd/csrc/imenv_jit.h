@@ -70,6 +70,9 @@ struct RolloutFlags {
 
 // Threads per block of the rollout kernel for this spec (0: does not fit LDS).
 int rollout_block_size(const SpecDev& d, const RolloutFlags& f);
+// Objective terms parked per thread in RolloutArgs::terms (trees with R > 1 retailers; 0: one replay
+// per row).
+int rollout_term_slots(const SpecDev& d, const RolloutFlags& f);
 std::string jit_rollout_source(const SpecDev& d, int maxc, const RolloutFlags& f, int bs);
 bool jit_rollout_load(const SpecDev& d, int maxc, const RolloutFlags& f, const std::string& arch, JitKernel& out,
                       std::string& msg);

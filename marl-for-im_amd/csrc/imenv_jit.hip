@@ -428,6 +428,16 @@ hipError_t jit_launch(const JitKernel& k, hipStream_t st, const SpecDev* sp, con
 }
 
 // ---------------------------------------------------------------- fused base-stock rollout
+int rollout_term_slots(const SpecDev& d, const RolloutFlags& f) {
+  // trees with R > 1 retailer rows: park rows 1..R-1 of the objective's terms in a global scratch and
+  // run the episode once (rollout_body TBUF); 0 = replay once per row (IMENV_ROLLOUT_REPLAY=1 forces
+  // it, for A/B)
+  if (!f.objective || d.s.num_retailers <= 1) return 0;
+  if (const char* v = std::getenv("IMENV_ROLLOUT_REPLAY"))
+    if (std::atoi(v) != 0) return 0;
+  return (d.s.num_retailers - 1) * d.s.num_periods;
+}
+
 int rollout_block_size(const SpecDev& d, const RolloutFlags&) {
   // LDS per block: the in-transit queue (int32 per slot per thread), the Poisson table, the pmf
   // weights and the reduction scratch. 256 threads unless the queue is long.
@@ -445,6 +455,7 @@ std::string jit_rollout_source(const SpecDev& d, int maxc, const RolloutFlags& f
   std::ostringstream o;
   emit_policy(o, d, maxc, false, jf, bs, 1);
   const int pmf = f.objective ? kRolloutPmfLds : 1;
+  const int tb = rollout_term_slots(d, f);
   o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
        "imenv_rollout_jit(const imenv::SpecDev* __restrict__ sp, const imenv::RolloutArgs A) {\n"
        "  __shared__ uint32_t s_thr["
@@ -460,7 +471,7 @@ std::string jit_rollout_source(const SpecDev& d, int maxc, const RolloutFlags& f
        "  __shared__ double s_red[JitSpec::BS / 64];\n"
        "  const JitSpec p(sp, A);\n"
        "  imenv::rollout_body<JitSpec, "
-    << blit(f.objective) << ">(p, A, sp, s_thr, s_guide, s_ring, s_pmf, " << pmf
+    << blit(f.objective) << ", " << tb << ">(p, A, sp, s_thr, s_guide, s_ring, s_pmf, " << pmf
     << ", s_red);\n"
        "}\n";
   return o.str();
@@ -477,8 +488,8 @@ bool jit_rollout_load(const SpecDev& d, int maxc, const RolloutFlags& f, const s
   if (!load_module(src, arch, "imenv_rollout_jit", out, msg)) return false;
   out.bs = bs;
   char tag[160];
-  std::snprintf(tag, sizeof tag, "jit:imenv_rollout_jit[N=%d,MC=%d,es=%d,flags=0x%x,bs=%d,%zuB,dev=%08x]",
-                d.s.num_nodes, maxc, d.es, f.key(), bs, src.size(), device_src_hash());
+  std::snprintf(tag, sizeof tag, "jit:imenv_rollout_jit[N=%d,MC=%d,es=%d,flags=0x%x,bs=%d,tb=%d,%zuB,dev=%08x]",
+                d.s.num_nodes, maxc, d.es, f.key(), bs, rollout_term_slots(d, f), src.size(), device_src_hash());
   out.tag = tag;
   return true;
 }

@@ -52,6 +52,22 @@ def test_rollout_matches_reference_golden(name):
     ro.close()
 
 
+@pytest.mark.parametrize("name", [c for c in ROLL if META[c]["kind"] in ("IM_div", "MAIM_div")])
+@pytest.mark.parametrize("replay", ["0", "1"])
+def test_tree_objective_single_pass_and_replay(name, replay, monkeypatch):
+    """Trees (R > 1 retailer rows): the single-pass kernel parks rows 1..R-1 of the objective's terms
+    (tb > 0) and the replay kernel re-runs the episode per row (IMENV_ROLLOUT_REPLAY=1, tb=0); both
+    give the reference's np.sum order bit for bit."""
+    monkeypatch.setenv("IMENV_ROLLOUT_REPLAY", replay)
+    m, d = META[name], CASES[name]
+    ro = _rollout(m["kind"], m["config"])
+    out = ro.run(d["policies"], demand=d["demand"])
+    for k in STATS:
+        np.testing.assert_array_equal(out[k].cpu().numpy(), d[k], err_msg="%s %s" % (name, k))
+    assert (",tb=0," in ro.kernel_info()) == (replay == "1"), ro.kernel_info()
+    ro.close()
+
+
 def test_dfo_func_and_powell_drop_in():
     """imenv.policy.dfo_func / optimize_inventory_policy on the InvManagement adaptor reproduce the
     reference's objective and its whole Powell search (inv_management.py:217-218)."""
