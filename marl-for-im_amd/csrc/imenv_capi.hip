@@ -56,16 +56,19 @@ __global__ void __launch_bounds__(256) imenv_reset_kernel(const SpecDev* __restr
   }
 }
 
-// packed [n][np] state rows -> int32 [N][n] SoA (imenv_get_state). part: 0 the value itself, 1 its
-// positive part (inventory from the net row), 2 its negative part (backlog from the net row)
-template <typename ST>
-__global__ void __launch_bounds__(256) imenv_unpack_kernel(const ST* __restrict__ src, int32_t* __restrict__ dst,
-                                                           int64_t n, int np, int N, int part) {
+// packed [n][np] state rows -> int32 [N][n] SoA (imenv_get_state): inventory and backlog are the
+// positive and negative parts of the signed net row, order_u its own row; one pass over both rows
+template <typename SN, typename ST>
+__global__ void __launch_bounds__(256) imenv_state_kernel(const SN* __restrict__ net, const ST* __restrict__ ou,
+                                                          int32_t* __restrict__ inv_out, int32_t* __restrict__ bl_out,
+                                                          int32_t* __restrict__ ou_out, int64_t n, int np, int N) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   for (int i = 0; i < N; ++i) {
-    const int32_t v = (int32_t)src[e * np + i];
-    dst[i * n + e] = part == 0 ? v : (part == 1 ? max(v, 0) : max(-v, 0));
+    const int32_t v = (int32_t)net[e * np + i];
+    if (inv_out) inv_out[i * n + e] = max(v, 0);
+    if (bl_out) bl_out[i * n + e] = max(-v, 0);
+    if (ou_out) ou_out[i * n + e] = (int32_t)ou[e * np + i];
   }
 }
 
@@ -106,34 +109,68 @@ __global__ void __launch_bounds__(256) imenv_rollout_stats_kernel(const double* 
   }
 }
 
-// np.mean / np.std (population) of every column of a row-major [rows][cols] float64 matrix: one block
-// per column, the two-pass form np.std uses (mean, then the mean of squared deviations); strided
-// per-thread sums, wavefront shuffles and a fixed wave order (deterministic).
-__global__ void __launch_bounds__(256) imenv_column_stats_kernel(const double* __restrict__ x, int64_t rows,
-                                                                 int32_t cols, double* __restrict__ out) {
+// np.mean / np.std (population) of every column of a row-major [rows][cols] float64 matrix, in the
+// two-pass form np.std uses (the mean, then the mean of squared deviations). Each pass: a grid of
+// row-chunk blocks x 64-column tiles writes one partial sum per (chunk, column); a finalize kernel adds
+// the partials of each column in chunk order. Within a block, lane l of a wave reads column
+// c0 + l % cw of row l / cw (cw = the tile's columns, 64 / cw rows per wave step), so a wave moves
+// whole consecutive rows (512 B for 8 columns); lanes of one column and the 4 waves are combined
+// through LDS in a fixed order. Deterministic: the same bits for the same input and grid.
+template <bool SQ>
+__global__ void __launch_bounds__(256) imenv_colsum_partial_kernel(const double* __restrict__ x, int64_t rows,
+                                                                   int32_t cols, int64_t chunk,
+                                                                   const double* __restrict__ mean_sd,
+                                                                   double* __restrict__ part) {
+  __shared__ double s_acc[256];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c0 = blockIdx.y * 64;
+  const int cw = (cols - c0) < 64 ? (cols - c0) : 64;
+  const int rpw = 64 / cw;                        // rows per wave step
+  const bool active = lane < rpw * cw;
+  const int c = c0 + lane % cw;
+  const int64_t r0 = (int64_t)blockIdx.x * chunk;
+  const int64_t r1 = (r0 + chunk) < rows ? (r0 + chunk) : rows;
+  const double mu = (SQ && active) ? mean_sd[2 * c] : 0.0;
+  double acc = 0.0;
+  if (active) {
+    for (int64_t r = r0 + (int64_t)w * rpw + lane / cw; r < r1; r += 4 * rpw) {
+      const double v = x[r * cols + c];
+      if (SQ) {
+        const double d = v - mu;
+        acc += d * d;
+      } else {
+        acc += v;
+      }
+    }
+  }
+  s_acc[tid] = acc;
+  __syncthreads();
+  if (tid < cw) {
+    double sum = 0.0;
+    for (int q = 0; q < 4; ++q)
+      for (int k = 0; k < rpw; ++k) sum += s_acc[q * 64 + k * cw + tid];
+    part[(int64_t)blockIdx.x * cols + c0 + tid] = sum;
+  }
+}
+
+// one block per column: strided per-thread sums of the chunk partials, then the waves' sums in a fixed
+// order (the partials' loads are independent, so 256 threads keep them in flight)
+template <bool SQ>
+__global__ void __launch_bounds__(256) imenv_colsum_finalize_kernel(const double* __restrict__ part, int64_t nb,
+                                                                    int64_t rows, int32_t cols,
+                                                                    double* __restrict__ out) {
   __shared__ double s_w[4];
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
-  auto block_sum = [&](double v) {
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    if ((tid & 63) == 0) s_w[tid >> 6] = v;
-    __syncthreads();
-    const double r = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);
-    __syncthreads();
-    return r;
-  };
-  double a = 0.0;
-  for (int64_t r = tid; r < rows; r += 256) a += x[r * cols + c];
-  const double mean = block_sum(a) / (double)rows;
-  double q = 0.0;
-  for (int64_t r = tid; r < rows; r += 256) {
-    const double d = x[r * cols + c] - mean;
-    q += d * d;
-  }
-  const double var = block_sum(q) / (double)rows;
+  double v = 0.0;
+  for (int64_t b = tid; b < nb; b += 256) v += part[b * cols + c];
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((tid & 63) == 0) s_w[tid >> 6] = v;
+  __syncthreads();
   if (tid == 0) {
-    out[2 * c] = mean;
-    out[2 * c + 1] = sqrt(var);
+    const double sum = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);
+    if (SQ) out[2 * c + 1] = sqrt(sum / (double)rows);
+    else out[2 * c] = sum / (double)rows;
   }
 }
 
@@ -170,6 +207,60 @@ __global__ void __launch_bounds__(256) imenv_cc_obs_kernel(const OT* __restrict_
       v = obs[(e * N + m) * F + (j - (N - 1) * (F + 1))];
     }
     out[q] = v;
+  }
+}
+
+// The same rows, one thread per (env, agent) row: a block of E = 256 / N envs stages its obs [E][N][F]
+// and clipped actions in LDS with coalesced loads, each thread assembles its row of N*F + N - 1 values
+// in an LDS slab (odd row stride: no bank conflicts), and the block writes the slab, which is one
+// contiguous run of the output, with 16-byte stores. Used when the slab fits 48 KiB.
+template <typename OT, typename AT>
+__global__ void __launch_bounds__(256) imenv_cc_obs_slab_kernel(const OT* __restrict__ obs, const AT* __restrict__ act,
+                                                                int64_t n, int N, int F, double lo, double hi,
+                                                                OT* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
+  const int W = N * F + N - 1;
+  const int WP = W | 1;                               // odd stride
+  const int E = 256 / N;
+  const int tid = threadIdx.x;
+  const int64_t e0 = (int64_t)blockIdx.x * E;
+  const int ne = (n - e0) < E ? (int)(n - e0) : E;
+  double* s_act = reinterpret_cast<double*>(s_raw);                       // [E][N]
+  OT* s_obs = reinterpret_cast<OT*>(s_act + E * N);                       // [E][N][F]
+  OT* s_out = s_obs + E * N * F;                                          // [E * N][WP]
+  for (int q = tid; q < ne * N * F; q += 256) s_obs[q] = obs[e0 * N * F + q];
+  for (int q = tid; q < ne * N; q += 256)
+    s_act[q] = act ? fmin(fmax((double)act[e0 * N + q], lo), hi) : 0.0;
+  __syncthreads();
+  if (tid < ne * N) {
+    const int el = tid / N, m = tid - el * N;
+    OT* row = s_out + tid * WP;
+    const OT* eo = s_obs + el * N * F;
+    int k = 0;
+    for (int o = 0; o < N; ++o)
+      if (o != m) row[k++] = (OT)s_act[el * N + o];     // opponent_action
+    for (int o = 0; o < N; ++o)
+      if (o != m)
+        for (int f = 0; f < F; ++f) row[k++] = eo[o * F + f];   // opponent_obs
+    for (int f = 0; f < F; ++f) row[k++] = eo[m * F + f];      // own_obs
+  }
+  __syncthreads();
+  const int total = ne * N * W;
+  OT* g = out + e0 * N * W;
+  constexpr int V = 16 / (int)sizeof(OT);            // values per 16-byte store
+  if (total % V == 0 && (reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+    for (int q = tid; q < total / V; q += 256) {
+      OT v[V];
+#pragma unroll
+      for (int u = 0; u < V; ++u) {
+        const int i = q * V + u;
+        v[u] = WP == W ? s_out[i] : s_out[(i / W) * WP + i % W];
+      }
+      if constexpr (V == 4) reinterpret_cast<float4*>(g)[q] = make_float4(v[0], v[1], v[2], v[3]);
+      else reinterpret_cast<double2*>(g)[q] = make_double2(v[0], v[1]);
+    }
+  } else {
+    for (int i = tid; i < total; i += 256) g[i] = WP == W ? s_out[i] : s_out[(i / W) * WP + i % W];
   }
 }
 
@@ -845,9 +936,23 @@ int imenv_set_episode_metrics(ImEnv* h, double* acc) {
 int imenv_column_stats(const double* x, int64_t rows, int32_t cols, double* out, void* stream) {
   if (!x || !out) return fail(IMENV_E_INVALID, "null argument");
   if (rows < 1 || cols < 1 || cols > 65535) return fail(IMENV_E_INVALID, "rows >= 1 and 1 <= cols <= 65535");
-  hipLaunchKernelGGL(imenv_column_stats_kernel, dim3((unsigned)cols), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     x, rows, cols, out);
-  HIPCHK(hipGetLastError());
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // row chunks: up to 1024 blocks per column tile, at most 2^20 partials, at least 256 rows per chunk
+  int64_t nb = std::min<int64_t>(1024, std::max<int64_t>(1, (int64_t(1) << 20) / cols));
+  nb = std::min<int64_t>(nb, (rows + 255) / 256);
+  const int64_t chunk = (rows + nb - 1) / nb;
+  nb = (rows + chunk - 1) / chunk;
+  double* part = nullptr;   // stream-ordered scratch (capturable), returned to the pool after the last use
+  HIPCHK(hipMallocAsync(reinterpret_cast<void**>(&part), (size_t)nb * cols * sizeof(double), st));
+  const dim3 g((unsigned)nb, (unsigned)((cols + 63) / 64)), b(256);
+  const dim3 gf((unsigned)cols), bf(256);
+  hipLaunchKernelGGL(imenv_colsum_partial_kernel<false>, g, b, 0, st, x, rows, cols, chunk, out, part);
+  hipLaunchKernelGGL(imenv_colsum_finalize_kernel<false>, gf, bf, 0, st, part, nb, rows, cols, out);
+  hipLaunchKernelGGL(imenv_colsum_partial_kernel<true>, g, b, 0, st, x, rows, cols, chunk, out, part);
+  hipLaunchKernelGGL(imenv_colsum_finalize_kernel<true>, gf, bf, 0, st, part, nb, rows, cols, out);
+  const hipError_t e = hipGetLastError();
+  (void)hipFreeAsync(part, st);
+  if (e != hipSuccess) return fail(IMENV_E_HIP, std::string("column stats: ") + hipGetErrorString(e));
   return IMENV_OK;
 }
 
@@ -859,6 +964,30 @@ int imenv_cc_observation(int64_t n, int32_t num_agents, int32_t num_features, co
   if ((obs_dtype != IMENV_F32 && obs_dtype != IMENV_F64) || (action_dtype != IMENV_F32 && action_dtype != IMENV_F64))
     return fail(IMENV_E_INVALID, "bad dtype");
   hipStream_t st = static_cast<hipStream_t>(stream);
+  {
+    // staged (env, agent)-row kernel when the block's slab fits 48 KiB
+    const int N = num_agents, F = num_features, W = N * F + N - 1, E = 256 / N;
+    const size_t osz = obs_dtype == IMENV_F64 ? 8 : 4;
+    const size_t lds = (size_t)E * N * 8 + (size_t)E * N * F * osz + (size_t)E * N * (W | 1) * osz;
+    if (N <= 256 && lds <= 48 * 1024) {
+      const dim3 g((unsigned)((n + E - 1) / E)), b(256);
+      if (obs_dtype == IMENV_F32 && action_dtype == IMENV_F32)
+        hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<float, float>), g, b, lds, st, static_cast<const float*>(obs),
+                           static_cast<const float*>(actions), n, N, F, clip_lo, clip_hi, static_cast<float*>(out));
+      else if (obs_dtype == IMENV_F32)
+        hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<float, double>), g, b, lds, st, static_cast<const float*>(obs),
+                           static_cast<const double*>(actions), n, N, F, clip_lo, clip_hi, static_cast<float*>(out));
+      else if (action_dtype == IMENV_F32)
+        hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<double, float>), g, b, lds, st, static_cast<const double*>(obs),
+                           static_cast<const float*>(actions), n, N, F, clip_lo, clip_hi, static_cast<double*>(out));
+      else
+        hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<double, double>), g, b, lds, st,
+                           static_cast<const double*>(obs), static_cast<const double*>(actions), n, N, F, clip_lo,
+                           clip_hi, static_cast<double*>(out));
+      HIPCHK(hipGetLastError());
+      return IMENV_OK;
+    }
+  }
   const int64_t total = n * num_agents * (int64_t)(num_agents * num_features + num_agents - 1);
   int64_t blocks = (total + 255) / 256;
   if (blocks > 65536) blocks = 65536;
@@ -933,24 +1062,18 @@ int imenv_get_state(ImEnv* h, int32_t* inv, int32_t* backlog, int32_t* order_u, 
   } else {
     const unsigned grid = (unsigned)((h->n + 255) / 256);
     // inventory and backlog are the two sides of the signed net row (imenv_device.h, NetOf)
-    void* src[3] = {h->d_net, h->d_net, h->d_ou};
-    int32_t* dst[3] = {inv, backlog, order_u};
-    for (int k = 0; k < 3; ++k) {
-      if (!dst[k]) continue;
-      const int part = k == 0 ? 1 : (k == 1 ? 2 : 0);
-      if (h->host.es == 1 && k < 2)
-        hipLaunchKernelGGL(imenv_unpack_kernel<int8_t>, dim3(grid), dim3(256), 0, st,
-                           static_cast<const int8_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes, part);
-      else if (h->host.es == 1)
-        hipLaunchKernelGGL(imenv_unpack_kernel<uint8_t>, dim3(grid), dim3(256), 0, st,
-                           static_cast<const uint8_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes, part);
-      else if (h->host.es == 2)
-        hipLaunchKernelGGL(imenv_unpack_kernel<int16_t>, dim3(grid), dim3(256), 0, st,
-                           static_cast<const int16_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes, part);
-      else
-        hipLaunchKernelGGL(imenv_unpack_kernel<int32_t>, dim3(grid), dim3(256), 0, st,
-                           static_cast<const int32_t*>(src[k]), dst[k], h->n, h->host.np, s.num_nodes, part);
-    }
+    if (h->host.es == 1)
+      hipLaunchKernelGGL((imenv_state_kernel<int8_t, uint8_t>), dim3(grid), dim3(256), 0, st,
+                         static_cast<const int8_t*>(h->d_net), static_cast<const uint8_t*>(h->d_ou), inv, backlog,
+                         order_u, h->n, h->host.np, s.num_nodes);
+    else if (h->host.es == 2)
+      hipLaunchKernelGGL((imenv_state_kernel<int16_t, int16_t>), dim3(grid), dim3(256), 0, st,
+                         static_cast<const int16_t*>(h->d_net), static_cast<const int16_t*>(h->d_ou), inv, backlog,
+                         order_u, h->n, h->host.np, s.num_nodes);
+    else
+      hipLaunchKernelGGL((imenv_state_kernel<int32_t, int32_t>), dim3(grid), dim3(256), 0, st,
+                         static_cast<const int32_t*>(h->d_net), static_cast<const int32_t*>(h->d_ou), inv, backlog,
+                         order_u, h->n, h->host.np, s.num_nodes);
     HIPCHK(hipGetLastError());
   }
   if (period) *period = h->t;
