@@ -86,7 +86,7 @@ struct StepArgs {
   void* net;                  // net inventory rows: inv - backlog (NetOf<ST>; see Row below)
   void* ou;
   void* ring;
-  int32_t* carry;
+  void* carry;                // noisy-delay carry rows (CarryOf<ST>)
   int32_t* bto;
   void* hist_d;
   void* hist_o;
@@ -291,18 +291,26 @@ __device__ __forceinline__ void store_words(void* __restrict__ p, const uint32_t
   }
 }
 
-// A packed row is NP elements of ST at base + e*NP. EXACT rows (N == NT) move as whole
-// 4/8/16-byte words (one vector instruction per lane); padded rows element-wise. Both forms
-// deliver raw words; unpack() turns them into ints.
+// A packed row is N elements of ST padded to a 4-byte multiple (row_len), at base + e*row_len. EXACT
+// rows (N == NT) move as whole 4/8/16-byte words (one vector instruction per lane); padded rows
+// element-wise. Both forms use the same stride for a given N and element type, so kernels of either
+// form can continue each other's episode. Both deliver raw words; unpack() turns them into ints.
+template <int ES>
+__host__ __device__ constexpr int row_len(int N) {
+  return ES == 1 ? ((N + 3) & ~3) : (ES == 2 ? ((N + 1) & ~1) : N);
+}
+
 template <typename ST, int NT, bool EXACT>
 struct Row {
   static constexpr int ES = (int)sizeof(ST);
-  static constexpr int NPT = ES == 1 ? ((NT + 3) & ~3) : (ES == 2 ? ((NT + 1) & ~1) : NT);
+  static constexpr int NPT = row_len<ES>(NT);
   static constexpr int BYTES = NPT * (int)sizeof(ST);
   static constexpr int WORDS = BYTES / 4;
 
-  __device__ static __forceinline__ void load(const ST* __restrict__ base, int64_t e, int np, int N,
+  // (the np argument is unused: the stride is row_len<ES>(N), the same for every row of one type)
+  __device__ static __forceinline__ void load(const ST* __restrict__ base, int64_t e, int /*np*/, int N,
                                               uint32_t (&w)[WORDS]) {
+    const int np = row_len<ES>(N);
     if (EXACT || np == NPT) {
       load_words<BYTES>(base + e * NPT, w);
     } else {
@@ -335,7 +343,9 @@ struct Row {
     unpack(w, v);
   }
 
-  __device__ static __forceinline__ void store(ST* __restrict__ base, int64_t e, int np, int N, const int (&v)[NT]) {
+  __device__ static __forceinline__ void store(ST* __restrict__ base, int64_t e, int /*np*/, int N,
+                                               const int (&v)[NT]) {
+    const int np = row_len<ES>(N);
     if (EXACT || np == NPT) {
       uint32_t w[WORDS];
 #pragma unroll
@@ -363,6 +373,11 @@ struct Row {
 // when a bound does not fit it).
 template <typename ST> struct NetOf { using type = ST; };
 template <> struct NetOf<uint8_t> { using type = int8_t; };
+// The noisy-delay carry (arrivals deferred to the next period; a deferral can defer earlier ones again,
+// so up to T shipments) is int16 beside uint8 / int16 state, int32 beside int32 state
+// (validate_and_derive widens the state type when T x the state bound exceeds int16).
+template <typename ST> struct CarryOf { using type = int16_t; };
+template <> struct CarryOf<int32_t> { using type = int32_t; };
 
 // ---------------------------------------------------------------- runtime spec policy
 // Every accessor reads the spec from device memory (scalar loads). Per-call flags come from A.
@@ -703,8 +718,9 @@ template <class P>
 struct StepLoad {
   using R = Row<typename P::ST, P::NT, P::EXACT>;
   using R32 = Row<int32_t, P::NT, P::EXACT>;
+  using RC = Row<typename CarryOf<typename P::ST>::type, P::NT, P::EXACT>;
   uint32_t aw[2 * P::NT];
-  uint32_t w_net[R::WORDS], w_ou[R::WORDS], w_cin[R32::WORDS], w_bto[R32::WORDS];
+  uint32_t w_net[R::WORDS], w_ou[R::WORDS], w_cin[RC::WORDS], w_bto[R32::WORDS];
   typename P::ST r_arr[P::NT];
   int cdem[P::NT];
   double du[P::NT];
@@ -730,13 +746,15 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
   const SN* __restrict__ p_net = static_cast<const SN*>(A.net);
   const ST* __restrict__ p_ou = static_cast<const ST*>(A.ou);
   const ST* __restrict__ p_ring = static_cast<const ST*>(A.ring);
-  const int32_t* __restrict__ p_carry = A.carry;
+  using CT = typename CarryOf<ST>::type;
+  using RC = Row<CT, NT, EXACT>;
+  const CT* __restrict__ p_carry = static_cast<const CT*>(A.carry);
   const int32_t* __restrict__ p_bto = A.bto;
   // ================= (A) loads: raw words only, every independent load issued before any use
   uint32_t (&aw)[2 * NT] = L.aw;
   uint32_t (&w_net)[R::WORDS] = L.w_net;
   uint32_t (&w_ou)[R::WORDS] = L.w_ou;
-  uint32_t (&w_cin)[R32::WORDS] = L.w_cin;
+  uint32_t (&w_cin)[RC::WORDS] = L.w_cin;
   uint32_t (&w_bto)[R32::WORDS] = L.w_bto;
   ST (&r_arr)[NT] = L.r_arr;
   int (&cdem)[NT] = L.cdem;
@@ -749,7 +767,9 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
 #pragma unroll
   for (int q = 0; q < R::WORDS; ++q) w_net[q] = w_ou[q] = 0;
 #pragma unroll
-  for (int q = 0; q < R32::WORDS; ++q) w_cin[q] = w_bto[q] = 0;
+  for (int q = 0; q < RC::WORDS; ++q) w_cin[q] = 0;
+#pragma unroll
+  for (int q = 0; q < R32::WORDS; ++q) w_bto[q] = 0;
 #pragma unroll
   for (int i = 0; i < NT; ++i) { cdem[i] = 0; du[i] = 1.0; r_arr[i] = 0; }
   {
@@ -782,7 +802,7 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
 #pragma unroll
     for (int i = 0; i < NT; ++i)
       if (i < N) r_arr[i] = p_ring[(int64_t)A.ring_row[i] * n + el];
-    if (p.noisy_delay()) R32::load(p_carry, el, np, N, w_cin);
+    if (p.noisy_delay()) RC::load(p_carry, el, np, N, w_cin);
     if (MC > 0) R32::load(p_bto, el, np, N, w_bto);
     if (p.demand_layout() == IMENV_LAYOUT_PER_ENV) {
 #pragma unroll
@@ -850,13 +870,15 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   SN* __restrict__ p_net = static_cast<SN*>(A.net);
   ST* __restrict__ p_ou = static_cast<ST*>(A.ou);
   ST* __restrict__ p_ring = static_cast<ST*>(A.ring);
-  int32_t* __restrict__ p_carry = A.carry;
+  using CT = typename CarryOf<ST>::type;
+  using RC = Row<CT, NT, EXACT>;
+  CT* __restrict__ p_carry = static_cast<CT*>(A.carry);
   int32_t* __restrict__ p_bto = A.bto;
   const int64_t ring_rows = n * np;   // elements per packed-row array (history)
   const uint32_t (&aw)[2 * NT] = L.aw;
   const uint32_t (&w_net)[R::WORDS] = L.w_net;
   const uint32_t (&w_ou)[R::WORDS] = L.w_ou;
-  const uint32_t (&w_cin)[R32::WORDS] = L.w_cin;
+  const uint32_t (&w_cin)[RC::WORDS] = L.w_cin;
   const uint32_t (&w_bto)[R32::WORDS] = L.w_bto;
   const ST (&r_arr)[NT] = L.r_arr;
   const int (&cdem)[NT] = L.cdem;
@@ -921,7 +943,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   R::unpack(w_ou, ou);
 #pragma unroll
   for (int i = 0; i < NT; ++i) arr[i] = (int)r_arr[i];
-  R32::unpack(w_cin, cin);
+  RC::unpack(w_cin, cin);
   R32::unpack(w_bto, btoc);
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
@@ -976,7 +998,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
 #pragma unroll
     for (int i = 0; i < NT; ++i)
       if (i < N) p_ring[(int64_t)A.ring_row[i] * n + e] = (ST)push[i];
-    if (p.noisy_delay()) R32::store(p_carry, e, np, N, cout);
+    if (p.noisy_delay()) RC::store(p_carry, e, np, N, cout);
     if (MC > 0) R32::store(p_bto, e, np, N, btoc);
     if (!split_ok) {          // no-return atomics
       atomicOr(A.err + e, 1u);

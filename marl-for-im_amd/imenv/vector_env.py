@@ -59,6 +59,7 @@ class VectorInvEnv:
         self._keep = []
         self._done = c_int32(0)
         self._done_ref = byref(self._done)
+        self.noisy_delay = bool(self.spec.noisy_delay)   # latched by reset(noisy_delay=True), as the C handle
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
@@ -144,6 +145,7 @@ class VectorInvEnv:
                                        uptr, ep, obs.data_ptr(), self._obs_code(obs.dtype), self._stream()),
                   "imenv_reset")
         self._keep = keep          # the copies are stream-ordered; keep sources alive one call
+        self.noisy_delay = self.noisy_delay or bool(noisy_delay)
         self.period = 0
         self.episode = self.episode + 1 if episode is None else int(episode)
         return obs
@@ -264,12 +266,16 @@ class VectorInvEnv:
         split = any(len(c) > 1 for c in s.children)
         hist = any(g in (nat.G_DEMAND_HIST, nat.G_ORDER_HIST) and j >= 1 for g, j in s.features)
         per = []
+        # noisy-delay carry rows: int16 beside uint8 / int16 state, else int32, padded to 4 bytes
+        # (CarryOf / row_len in imenv_device.h); divergent backlog_to rows: int32 [N]
+        cb = 2 if es < 4 else 4
+        carry_row = cb * (((N + 1) & ~1) if cb == 2 else N)
         for t in range(T):
             b = N * action_bytes + 2 * NP * es + (2 * NP * es if t > 0 else 0)
             b += es * sum(1 for i in range(N) if t >= d[i]) + N * es
-            for rows in (s.noisy_delay, split):
-                if rows:
-                    b += 4 * NP + (4 * NP if t > 0 else 0)
+            for on, row in ((self.noisy_delay, carry_row), (split, 4 * N)):
+                if on:
+                    b += row + (row if t > 0 else 0)
             if hist:
                 b += 2 * NP * es
             for g, j in s.features:

@@ -303,6 +303,42 @@ def test_gpu_ragged_env_counts(kind, cfg, odt):
         env.close()
 
 
+IM10 = dict(num_stages=10, num_periods=30, init_inv=np.ones(10) * 10, inv_target=np.zeros(10),
+            inv_max=np.ones(10) * 30, price=np.arange(11, 0, -1), stock_cost=np.full(10, 0.3),
+            backlog_cost=np.full(10, 0.6), delay=np.array([1, 2, 3, 1, 4, 2, 3, 1, 2, 2]), demand_dist="poisson",
+            mu=5, seed=52)
+
+
+@pytest.mark.parametrize("state_bytes", [None, "2", "4"])
+def test_gpu_jit_and_aot_continue_each_others_episode(state_bytes, monkeypatch):
+    """10 stages (the AOT kernel pads them to 16: element-wise rows) with noisy delay (int16 / int32
+    carry rows): the JIT and AOT kernels alternate step by step within one episode, so every packed
+    row (net inventory, order_u, carry) must have one layout for both. == oracle, in-kernel draws."""
+    if state_bytes:
+        monkeypatch.setenv("IMENV_STATE_BYTES", state_bytes)
+    n = 300
+    env = _env("IM", IM10, n, env_offset=5)
+    ora = OracleEnv("IM", IM10, n_envs=n)
+    for ep in range(2):
+        o_g = env.reset(noisy_delay=True, noisy_delay_threshold=0.4)
+        o_c = ora.reset(noisy_delay=True, noisy_delay_threshold=0.4,
+                        rng=dict(seed=52, episode=ep, env_offset=5, mu=5))
+        np.testing.assert_array_equal(o_g.cpu().numpy(), o_c.astype(np.float32))
+        rs = np.random.RandomState(ep)
+        for t in range(30):
+            env.set_jit((t + ep) % 2)
+            a = rs.uniform(-1, 1, size=(n, 10))
+            o_g, r_g, _, _ = env.step(torch.as_tensor(a, device=DEV))
+            o_c, r_c, _, _ = ora.step(a)
+            np.testing.assert_array_equal(o_g.cpu().numpy(), o_c.astype(np.float32), err_msg="ep %d t %d" % (ep, t))
+            np.testing.assert_array_equal(r_g.cpu().numpy(), r_c, err_msg="ep %d t %d" % (ep, t))
+            st = env.state()
+            for k in ("inv", "backlog", "order_u"):
+                np.testing.assert_array_equal(st[k].cpu().numpy(), ora.state_arrays()[k])
+        assert ("jit:" in env.kernel_info()) == ((29 + ep) % 2 == 1)
+    env.close()
+
+
 def test_gpu_step_traffic_matches_bench_formula():
     """Algorithmic bytes per env-step for the bench layouts: C2 96 B steady,
     95.5 B averaged over the 30-period episode (t = 0 reads no state rows, node i no arrival
