@@ -538,7 +538,7 @@ int validate_and_derive(const ImEnvSpec& s, SpecDev& d, int& maxc) {
   const int64_t bound = state_bound(s);
   d.es = bound <= 255 ? 1 : (bound <= 32767 ? 2 : 4);
   if (d.es == 1 && net_bound(s) > 127) d.es = 2;   // the net row is signed (int8 beside uint8 rows)
-  if (d.es < 4 && (int64_t)s.num_periods * bound > 32767) d.es = 4;   // int16 noisy-delay carry (CarryOf)
+  if (d.es == 1 && (int64_t)s.num_periods * bound > 32767) d.es = 2;   // int16 noisy-delay carry (CarryOf)
   if (const char* v = std::getenv("IMENV_STATE_BYTES")) {
     const int want = std::atoi(v);
     if ((want == 2 || want == 4) && want > d.es) d.es = want;

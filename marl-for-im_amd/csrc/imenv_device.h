@@ -374,10 +374,10 @@ struct Row {
 template <typename ST> struct NetOf { using type = ST; };
 template <> struct NetOf<uint8_t> { using type = int8_t; };
 // The noisy-delay carry (arrivals deferred to the next period; a deferral can defer earlier ones again,
-// so up to T shipments) is int16 beside uint8 / int16 state, int32 beside int32 state
-// (validate_and_derive widens the state type when T x the state bound exceeds int16).
-template <typename ST> struct CarryOf { using type = int16_t; };
-template <> struct CarryOf<int32_t> { using type = int32_t; };
+// so up to T shipments) is int16 beside uint8 state (validate_and_derive widens the state to int16
+// when T x the state bound exceeds int16), int32 beside int16 / int32 state.
+template <typename ST> struct CarryOf { using type = int32_t; };
+template <> struct CarryOf<uint8_t> { using type = int16_t; };
 
 // ---------------------------------------------------------------- runtime spec policy
 // Every accessor reads the spec from device memory (scalar loads). Per-call flags come from A.

@@ -266,9 +266,9 @@ class VectorInvEnv:
         split = any(len(c) > 1 for c in s.children)
         hist = any(g in (nat.G_DEMAND_HIST, nat.G_ORDER_HIST) and j >= 1 for g, j in s.features)
         per = []
-        # noisy-delay carry rows: int16 beside uint8 / int16 state, else int32, padded to 4 bytes
-        # (CarryOf / row_len in imenv_device.h); divergent backlog_to rows: int32 [N]
-        cb = 2 if es < 4 else 4
+        # noisy-delay carry rows: int16 beside uint8 state, else int32, padded to 4 bytes (CarryOf /
+        # row_len in imenv_device.h); divergent backlog_to rows: int32 [N]
+        cb = 2 if es == 1 else 4
         carry_row = cb * (((N + 1) & ~1) if cb == 2 else N)
         for t in range(T):
             b = N * action_bytes + 2 * NP * es + (2 * NP * es if t > 0 else 0)
