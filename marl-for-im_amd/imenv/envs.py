@@ -115,11 +115,36 @@ class _Adaptor:
         np.random.seed(seed=int(self.SEED))              # IM_env.py:46: the process-global stream
         self._setup_spaces()
         self._env = VectorInvEnv(sp, n_envs=1, device=device, obs_dtype=torch.float64)
+        self._step_buffers()
         self._uniform_order = ([N - 1] + list(range(N - 1))) if sp.serial else list(range(N))
         self.period = 0
         self.reset()
 
     # ------------------------------------------------------------------ construction helpers
+    def _step_buffers(self):
+        """Persistent buffers of the per-step round trip: everything step() returns is written by the
+        kernels into two device buffers (float64: obs | reward | profit; int32: order, demand,
+        acquisition, ship, ship_to, backlog_to, inv, backlog, order_u, split-guard flag), copied to
+        pinned host memory with two asynchronous copies and one synchronisation per step."""
+        N, F = self.num_nodes, self.spec.num_features
+        nr = N if self.spec.reward_mode == nat.REWARD_INDEPENDENT else 1
+        dev = self._env.device
+        self._dev_f = torch.empty(N * F + nr + N, dtype=torch.float64, device=dev)
+        self._dev_i = torch.empty(9 * N + 1, dtype=torch.int32, device=dev)
+        self._host_f = torch.empty(self._dev_f.shape, dtype=torch.float64, pin_memory=True)
+        self._host_i = torch.empty(self._dev_i.shape, dtype=torch.int32, pin_memory=True)
+        self._host_a = torch.empty((1, N), dtype=torch.float64, pin_memory=True)
+        self._dev_a = torch.empty((1, N), dtype=torch.float64, device=dev)
+        f, i = self._dev_f, self._dev_i
+        self._obs_v = f[:N * F].view(1, N, F)
+        self._rew_v = f[N * F:N * F + nr].view((1, N) if nr == N else (1,))
+        iv = lambda j: i[j * N:(j + 1) * N].view(1, N)
+        self._info_v = dict(order=iv(0), demand=iv(1), acquisition=iv(2), ship=iv(3),
+                            profit=f[N * F + nr:].view(1, N), ship_to=iv(4), backlog_to=iv(5))
+        self._state_v = [i[(6 + j) * N:(7 + j) * N].view(N, 1) for j in range(3)]
+        self._flag_v = i[9 * N:]
+        self._nr = nr
+
     def _tree_depth(self):
         depth = np.zeros(self.num_nodes, dtype=int)
         for i in range(1, self.num_nodes):
@@ -229,21 +254,25 @@ class _Adaptor:
                 if t - int(self.delay[i]) >= 0:
                     u[i] = np.random.uniform(0, 1)
             self._env.set_delay_uniforms(t, u[None, :])
-        obs, rew, _, info = self._env.step(torch.as_tensor(act[None, :], dtype=torch.float64), info=True)
-        st = self._env.state()
-        parts = [obs.reshape(-1), rew.reshape(-1)] + [info[k].reshape(-1).double() for k in
-                                                      ("order", "demand", "ship", "acquisition", "profit")] + \
-                [st[k].reshape(-1).double() for k in ("inv", "backlog", "order_u")]
-        host = torch.cat(parts).cpu().numpy()      # one device-to-host copy per step
+        self._host_a.numpy()[0] = act                 # pinned; the previous step's copies have completed
+        self._dev_a.copy_(self._host_a, non_blocking=True)
+        env = self._env
+        env.step(self._dev_a, obs_out=self._obs_v, reward_out=self._rew_v, info_out=self._info_v)
+        env.state(out=self._state_v)
+        if not self.serial:    # per-env split-guard flag into the int32 buffer (no separate round trip)
+            nat.check(env.lib.imenv_get_errors(env._h, self._flag_v.data_ptr(), None, env._stream()),
+                      "imenv_get_errors")
+        self._host_f.copy_(self._dev_f, non_blocking=True)
+        self._host_i.copy_(self._dev_i, non_blocking=True)
+        torch.cuda.current_stream(env.device).synchronize()
+        hf, hi = self._host_f.numpy(), self._host_i.numpy()
         F = self.spec.num_features
-        o = host[:N * F].reshape(N, F)
-        k = N * F
-        nr = rew.numel()
-        r = host[k:k + nr]
-        k += nr
-        order, dem, ship, acq, profit, inv, bl, ou = (host[k + j * N:k + (j + 1) * N] for j in range(8))
-        flags, anyv = self._env.errors() if not self.serial else (None, 0)
-        if anyv:
+        o = hf[:N * F].reshape(N, F).copy()
+        r = hf[N * F:N * F + self._nr].copy()
+        profit = hf[N * F + self._nr:].copy()
+        order, dem, acq, ship = (hi[j * N:(j + 1) * N] for j in range(4))
+        inv, bl, ou = (hi[(6 + j) * N:(7 + j) * N] for j in range(3))
+        if not self.serial and hi[9 * N]:
             raise Exception("Infinite Loop (divergent shipment split guard, IM_div_env.py:424-498)")
         self.order_r[t] = order
         self.demand[t] = dem
@@ -252,7 +281,7 @@ class _Adaptor:
         self.inv[t + 1] = inv
         self.backlog[t + 1] = bl
         self.order_u[t + 1] = ou
-        return self._finish(t, o, r, profit.copy())
+        return self._finish(t, o, r, profit)
 
     def close(self):
         self._env.close()

@@ -157,8 +157,12 @@ class VectorInvEnv:
                   "imenv_set_delay_uniforms")
         self._keep_u = t
 
-    def step(self, actions, obs_out=None, reward_out=None, info=False):
-        """step(action) (IM_env.py:287-360): actions [n, N] (or [n*N]) in the spec's action units."""
+    def step(self, actions, obs_out=None, reward_out=None, info=False, info_out=None):
+        """step(action) (IM_env.py:287-360): actions [n, N] (or [n*N]) in the spec's action units.
+
+        info=True returns the info tensors (order, demand, acquisition, ship, profit, ship_to,
+        backlog_to, each [n, N]); info_out: a dict of caller-owned contiguous tensors of those names
+        ([n, N], int32 / float64 profit) the kernel writes instead (no allocation per step)."""
         a = actions
         # fast path: a contiguous float device tensor of n*N values is passed as is
         if not (torch.is_tensor(a) and a.device == self.device and a.dtype in _FLOATS and a.is_contiguous() and
@@ -171,11 +175,16 @@ class VectorInvEnv:
         rew = self._out(reward_out, self.reward_shape(), (torch.float64,), "reward_out")
         inf = None
         iptr = None
-        if info:
-            z = lambda dt: torch.empty((self.n, self.N), dtype=dt, device=self.device)
-            inf = dict(order=z(torch.int32), demand=z(torch.int32), acquisition=z(torch.int32),
-                       ship=z(torch.int32), profit=z(torch.float64), ship_to=z(torch.int32),
-                       backlog_to=z(torch.int32))
+        if info or info_out is not None:
+            if info_out is not None:
+                inf = {k: self._out(info_out[k], (self.n, self.N),
+                                    (torch.float64 if k == "profit" else torch.int32,), "info_out[%s]" % k)
+                       for k in ("order", "demand", "acquisition", "ship", "profit", "ship_to", "backlog_to")}
+            else:
+                z = lambda dt: torch.empty((self.n, self.N), dtype=dt, device=self.device)
+                inf = dict(order=z(torch.int32), demand=z(torch.int32), acquisition=z(torch.int32),
+                           ship=z(torch.int32), profit=z(torch.float64), ship_to=z(torch.int32),
+                           backlog_to=z(torch.int32))
             ci = nat.ImEnvInfo(*[inf[k].data_ptr() for k in ("order", "demand", "acquisition", "ship",
                                                                "profit", "ship_to", "backlog_to")])
             iptr = byref(ci)
@@ -189,9 +198,13 @@ class VectorInvEnv:
         self.period += 1
         return obs, rew, bool(done.value), inf
 
-    def state(self):
-        """inv / backlog / order_u at the current period as [n, N] int32 (base_restock_policy.py:12)."""
-        bufs = [torch.empty((self.N, self.n), dtype=torch.int32, device=self.device) for _ in range(3)]
+    def state(self, out=None):
+        """inv / backlog / order_u at the current period as [n, N] int32 (base_restock_policy.py:12).
+        out: three caller-owned contiguous int32 [N, n] tensors to write instead (no allocation)."""
+        if out is not None:
+            bufs = [self._out(b, (self.N, self.n), (torch.int32,), "state out") for b in out]
+        else:
+            bufs = [torch.empty((self.N, self.n), dtype=torch.int32, device=self.device) for _ in range(3)]
         p = c_int32()
         nat.check(self.lib.imenv_get_state(self._h, bufs[0].data_ptr(), bufs[1].data_ptr(), bufs[2].data_ptr(),
                                            byref(p), self._stream()), "imenv_get_state")
