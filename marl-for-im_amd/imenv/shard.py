@@ -14,6 +14,9 @@ link. Fewer, larger collectives therefore win:
   t+1 on RCCL's stream (``async_op``); the send buffer is reused only after that collective completes.
 - ``EpisodeGather``: one collective per episode over the whole [T+1, n, ...] rollout. It moves 30x
   the bytes per call and makes 30x fewer calls.
+The evaluation harness's statistics over sharded test episodes need one small collective:
+``global_metrics_stats`` all-gathers each rank's (mean, std, count) per metric column and merges
+them (Chan et al.), so the mean / std are those of all envs on all ranks.
 """
 import torch
 import torch.distributed as dist
@@ -154,3 +157,42 @@ class EpisodeGather(PackedGather):
     def result(self):
         self.wait(0)
         return self.gathered(0)
+
+
+def merge_column_stats(stats, counts):
+    """Per-rank np.mean / np.std (population) of the same columns -> those of the union of the rows.
+
+    stats: [W, C, 2] (mean, std) per rank; counts: [W] rows per rank. Chan et al.'s pairwise update
+    in float64: M2 = sum_r (n_r std_r^2 + n_r (mean_r - mean)^2), mean = sum_r n_r mean_r / n."""
+    stats = torch.as_tensor(stats, dtype=torch.float64)
+    n_r = torch.as_tensor(counts, dtype=torch.float64).reshape(-1, 1)
+    n = n_r.sum()
+    mean = (n_r * stats[..., 0]).sum(0) / n
+    m2 = (n_r * stats[..., 1] ** 2 + n_r * (stats[..., 0] - mean) ** 2).sum(0)
+    return torch.stack([mean, torch.sqrt(m2 / n)], dim=-1)
+
+
+def gather_column_stats(local_stats, count, group=None):
+    """All-gather every rank's [C, 2] (mean, std) and row count (one collective of C*2+1 doubles) and
+    merge them: the evaluation harness's mean / std over the envs of all ranks
+    (inv_management.py:608-643 over the whole test set, when the test episodes are sharded)."""
+    ls = local_stats.to(torch.float64)
+    buf = torch.cat([ls.reshape(-1), torch.tensor([float(count)], dtype=torch.float64, device=ls.device)])
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty(world * buf.numel(), dtype=torch.float64, device=ls.device)
+        dist.all_gather_into_tensor(out, buf, group=group)
+        rows = out.view(world, -1)
+    else:
+        parts = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf, group=group)
+        rows = torch.stack(parts)
+    rows = rows.cpu()
+    C = ls.shape[0]
+    return merge_column_stats(rows[:, :-1].reshape(world, C, 2), rows[:, -1])
+
+
+def global_metrics_stats(env, group=None):
+    """np.mean / np.std of every evaluation-harness metric column over the envs of every rank
+    (VectorInvEnv.metrics_stats on each rank, then gather_column_stats)."""
+    return gather_column_stats(env.metrics_stats(), env.n, group)

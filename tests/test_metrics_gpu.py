@@ -65,3 +65,36 @@ def test_column_stats_large():
     xn = x.cpu().numpy()
     np.testing.assert_allclose(out[:, 0].cpu().numpy(), xn.mean(axis=0), rtol=1e-12)
     np.testing.assert_allclose(out[:, 1].cpu().numpy(), xn.std(axis=0), rtol=1e-12)
+
+
+def test_metric_stats_merge_over_shards():
+    """Harness stats of 3 env shards (env_offset, in-kernel draws) merged with imenv.shard's Chan merge
+    (what global_metrics_stats does over ranks) == the stats of one env over all envs, and == np.mean /
+    np.std of the per-env sums."""
+    from imenv import VectorInvEnv
+    from imenv.shard import merge_column_stats, shard_range
+    meta, _ = load_case("C2_MAIM4")
+    total = 10007
+
+    def run(n, off):
+        env = VectorInvEnv(meta["kind"], meta["config"], n_envs=n, device=DEV, env_offset=off)
+        env.attach_metrics()
+        env.reset()
+        g = torch.Generator(device=DEV)
+        for t in range(env.T):
+            g.manual_seed(t)
+            a = torch.rand((total, env.N), generator=g, device=DEV)[off:off + n] * 2 - 1
+            env.step(a.contiguous())
+        stats, m = env.metrics_stats(), env._metrics.clone()
+        env.close()
+        return stats, m
+
+    whole_stats, whole = run(total, 0)
+    parts = [run(c, o) for o, c in (shard_range(total, 3, r) for r in range(3))]
+    np.testing.assert_array_equal(torch.cat([m for _, m in parts]).cpu().numpy(), whole.cpu().numpy())
+    merged = merge_column_stats(torch.stack([s.cpu() for s, _ in parts]),
+                                [shard_range(total, 3, r)[1] for r in range(3)]).numpy()
+    x = whole.cpu().numpy()
+    np.testing.assert_allclose(merged[:, 0], x.mean(0), rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(merged[:, 1], x.std(0), rtol=1e-10, atol=1e-9)
+    np.testing.assert_allclose(merged, whole_stats.cpu().numpy(), rtol=1e-10, atol=1e-9)

@@ -15,7 +15,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from imenv.shard import StepGather, shard_range, weak_offset
+from imenv.shard import StepGather, gather_column_stats, merge_column_stats, shard_range, weak_offset
 
 C2 = dict(num_stages=4, num_periods=30, init_inv=np.ones(4) * 10, inv_target=np.zeros(4),
           inv_max=np.ones(4) * 30, price=np.array([5, 4, 3, 2, 1]),
@@ -159,3 +159,31 @@ def test_packed_step_and_episode_gathers(tmp_path):
     for rank in range(2):
         assert torch.equal(got["eo"][rank], base + rank)
         assert torch.equal(got["er"][rank], torch.full((T, n, N), -1.0 - rank, dtype=torch.float64))
+
+
+def _stats_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        x = np.random.RandomState(7).normal(10, 50, size=(1001, 8))       # every rank builds the same table
+        offset, count = shard_range(len(x), world, rank)
+        mine = torch.from_numpy(x[offset:offset + count])
+        local = torch.stack([mine.mean(0), mine.std(0, unbiased=False)], dim=-1)
+        got = gather_column_stats(local, count)
+        if rank == 0:
+            torch.save(dict(got=got), out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_metric_stats_over_ranks(tmp_path):
+    """The harness's np.mean / np.std over the envs of all ranks from per-rank stats (Chan merge)."""
+    out = str(tmp_path / "stats.pt")
+    mp.spawn(_stats_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)["got"].numpy()
+    x = np.random.RandomState(7).normal(10, 50, size=(1001, 8))
+    np.testing.assert_allclose(got[:, 0], x.mean(0), rtol=1e-12)
+    np.testing.assert_allclose(got[:, 1], x.std(0), rtol=1e-12)
+    # merging a single rank is the identity; empty-free uneven splits
+    one = merge_column_stats(torch.tensor([[[3.0, 2.0]]]), [5])
+    assert torch.allclose(one, torch.tensor([[3.0, 2.0]], dtype=torch.float64))
