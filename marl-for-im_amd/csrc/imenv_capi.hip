@@ -214,22 +214,22 @@ __global__ void __launch_bounds__(256) imenv_cc_obs_kernel(const OT* __restrict_
 // and clipped actions in LDS with coalesced loads, each thread assembles its row of N*F + N - 1 values
 // in an LDS slab (odd row stride: no bank conflicts), and the block writes the slab, which is one
 // contiguous run of the output, with 16-byte stores. Used when the slab fits 48 KiB.
-template <typename OT, typename AT>
-__global__ void __launch_bounds__(256) imenv_cc_obs_slab_kernel(const OT* __restrict__ obs, const AT* __restrict__ act,
-                                                                int64_t n, int N, int F, double lo, double hi,
-                                                                OT* __restrict__ out) {
+template <typename OT, typename AT, int BS>
+__global__ void __launch_bounds__(BS) imenv_cc_obs_slab_kernel(const OT* __restrict__ obs, const AT* __restrict__ act,
+                                                               int64_t n, int N, int F, double lo, double hi,
+                                                               OT* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
   const int W = N * F + N - 1;
   const int WP = W | 1;                               // odd stride
-  const int E = 256 / N;
+  const int E = BS / N;
   const int tid = threadIdx.x;
   const int64_t e0 = (int64_t)blockIdx.x * E;
   const int ne = (n - e0) < E ? (int)(n - e0) : E;
   double* s_act = reinterpret_cast<double*>(s_raw);                       // [E][N]
   OT* s_obs = reinterpret_cast<OT*>(s_act + E * N);                       // [E][N][F]
   OT* s_out = s_obs + E * N * F;                                          // [E * N][WP]
-  for (int q = tid; q < ne * N * F; q += 256) s_obs[q] = obs[e0 * N * F + q];
-  for (int q = tid; q < ne * N; q += 256)
+  for (int q = tid; q < ne * N * F; q += BS) s_obs[q] = obs[e0 * N * F + q];
+  for (int q = tid; q < ne * N; q += BS)
     s_act[q] = act ? fmin(fmax((double)act[e0 * N + q], lo), hi) : 0.0;
   __syncthreads();
   if (tid < ne * N) {
@@ -248,20 +248,50 @@ __global__ void __launch_bounds__(256) imenv_cc_obs_slab_kernel(const OT* __rest
   const int total = ne * N * W;
   OT* g = out + e0 * N * W;
   constexpr int V = 16 / (int)sizeof(OT);            // values per 16-byte store
+  const bool dense16 = WP == W && (reinterpret_cast<uintptr_t>(s_out) & 15) == 0;
   if (total % V == 0 && (reinterpret_cast<uintptr_t>(g) & 15) == 0) {
-    for (int q = tid; q < total / V; q += 256) {
+    for (int q = tid; q < total / V; q += BS) {
       OT v[V];
+      if (dense16) {                                // 16-byte LDS read of the same values
+        if constexpr (V == 4) {
+          const float4 x = reinterpret_cast<const float4*>(s_out)[q];
+          v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+        } else {
+          const double2 x = reinterpret_cast<const double2*>(s_out)[q];
+          v[0] = x.x; v[1] = x.y;
+        }
+      } else {
 #pragma unroll
-      for (int u = 0; u < V; ++u) {
-        const int i = q * V + u;
-        v[u] = WP == W ? s_out[i] : s_out[(i / W) * WP + i % W];
+        for (int u = 0; u < V; ++u) {
+          const int i = q * V + u;
+          v[u] = WP == W ? s_out[i] : s_out[(i / W) * WP + i % W];
+        }
       }
       if constexpr (V == 4) reinterpret_cast<float4*>(g)[q] = make_float4(v[0], v[1], v[2], v[3]);
       else reinterpret_cast<double2*>(g)[q] = make_double2(v[0], v[1]);
     }
   } else {
-    for (int i = tid; i < total; i += 256) g[i] = WP == W ? s_out[i] : s_out[(i / W) * WP + i % W];
+    for (int i = tid; i < total; i += BS) g[i] = WP == W ? s_out[i] : s_out[(i / W) * WP + i % W];
   }
+}
+
+template <int BS>
+void launch_cc_slab(dim3 g, size_t lds, hipStream_t st, const void* obs, int obs_dtype, const void* actions,
+                    int action_dtype, int64_t n, int N, int F, double lo, double hi, void* out) {
+  const dim3 b(BS);
+  if (obs_dtype == IMENV_F32 && action_dtype == IMENV_F32)
+    hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<float, float, BS>), g, b, lds, st, static_cast<const float*>(obs),
+                       static_cast<const float*>(actions), n, N, F, lo, hi, static_cast<float*>(out));
+  else if (obs_dtype == IMENV_F32)
+    hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<float, double, BS>), g, b, lds, st, static_cast<const float*>(obs),
+                       static_cast<const double*>(actions), n, N, F, lo, hi, static_cast<float*>(out));
+  else if (action_dtype == IMENV_F32)
+    hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<double, float, BS>), g, b, lds, st, static_cast<const double*>(obs),
+                       static_cast<const float*>(actions), n, N, F, lo, hi, static_cast<double*>(out));
+  else
+    hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<double, double, BS>), g, b, lds, st,
+                       static_cast<const double*>(obs), static_cast<const double*>(actions), n, N, F, lo, hi,
+                       static_cast<double*>(out));
 }
 
 // GAE over a [T][n] rollout (RLlib 1.5 compute_advantages with use_gae, as called by
@@ -967,24 +997,17 @@ int imenv_cc_observation(int64_t n, int32_t num_agents, int32_t num_features, co
   hipStream_t st = static_cast<hipStream_t>(stream);
   {
     // staged (env, agent)-row kernel when the block's slab fits 48 KiB
-    const int N = num_agents, F = num_features, W = N * F + N - 1, E = 256 / N;
+    int BSC = 256;                                    // IMENV_CC_BS=512: 512-thread blocks (tuning)
+    if (const char* v = std::getenv("IMENV_CC_BS")) BSC = std::atoi(v) == 512 ? 512 : 256;
+    const int N = num_agents, F = num_features, W = N * F + N - 1, E = BSC / N;
     const size_t osz = obs_dtype == IMENV_F64 ? 8 : 4;
     const size_t lds = (size_t)E * N * 8 + (size_t)E * N * F * osz + (size_t)E * N * (W | 1) * osz;
     if (N <= 256 && lds <= 48 * 1024) {
-      const dim3 g((unsigned)((n + E - 1) / E)), b(256);
-      if (obs_dtype == IMENV_F32 && action_dtype == IMENV_F32)
-        hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<float, float>), g, b, lds, st, static_cast<const float*>(obs),
-                           static_cast<const float*>(actions), n, N, F, clip_lo, clip_hi, static_cast<float*>(out));
-      else if (obs_dtype == IMENV_F32)
-        hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<float, double>), g, b, lds, st, static_cast<const float*>(obs),
-                           static_cast<const double*>(actions), n, N, F, clip_lo, clip_hi, static_cast<float*>(out));
-      else if (action_dtype == IMENV_F32)
-        hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<double, float>), g, b, lds, st, static_cast<const double*>(obs),
-                           static_cast<const float*>(actions), n, N, F, clip_lo, clip_hi, static_cast<double*>(out));
+      const dim3 g((unsigned)((n + E - 1) / E)), b(BSC);
+      if (BSC == 512)
+        launch_cc_slab<512>(g, lds, st, obs, obs_dtype, actions, action_dtype, n, N, F, clip_lo, clip_hi, out);
       else
-        hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<double, double>), g, b, lds, st,
-                           static_cast<const double*>(obs), static_cast<const double*>(actions), n, N, F, clip_lo,
-                           clip_hi, static_cast<double*>(out));
+        launch_cc_slab<256>(g, lds, st, obs, obs_dtype, actions, action_dtype, n, N, F, clip_lo, clip_hi, out);
       HIPCHK(hipGetLastError());
       return IMENV_OK;
     }
