@@ -35,6 +35,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "env-steps/sec (whole node), 4-stage × 2^20 envs; % HBM roofline"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E (spec)
+CPU_SHARE = 16             # host cores per GPU on the GPU box (worker pools must stay within it)
 
 C2_CONFIG = dict(num_stages=4, num_periods=30, init_inv=np.ones(4) * 10, inv_target=np.zeros(4),
                  inv_max=np.ones(4) * 30, price=np.array([5, 4, 3, 2, 1]),
@@ -103,7 +104,10 @@ def cpu_baseline(seconds=1.5, cname="C2"):
 
 
 def _cpu_baseline_here(seconds, cname):
-    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    # the GPU box's CPU share is 16 cores per GPU (os.cpu_count() there reports the whole host, many
+    # times that, and larger pools are refused); both numbers go into the sample text
+    visible = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cores = max(1, min(CPU_SHARE, visible))
     ctx = mp.get_context("fork")   # before any GPU call in this process: plain fork, no exec
     with ctx.Pool(cores) as pool:
         res = pool.map(_cpu_worker, [(seconds, 100 + i, cname) for i in range(cores)])
@@ -111,8 +115,10 @@ def _cpu_baseline_here(seconds, cname):
     return dict(value=round(total, 1), unit="env-steps/s", cores=cores, kind="port",
                 sample="oracle/im_oracle.py %s (%s config), 1 env per process, %d processes x "
                        "%.1f s of whole 30-period episodes each (%d env-steps total), host-fed Poisson(5) demand, "
-                       "BLAS threads 1; per core %.0f env-steps/s" % (CONFIGS[cname][0], cname, cores, seconds,
-                                                                     sum(s for s, _ in res), total / cores))
+                       "BLAS threads 1; per core %.0f env-steps/s; pool capped at the box's %d-core CPU share "
+                       "per GPU (host reports %d visible, %d total)"
+                       % (CONFIGS[cname][0], cname, cores, seconds, sum(s for s, _ in res), total / cores,
+                          CPU_SHARE, visible, os.cpu_count()))
 
 
 # ----------------------------------------------------------------- PMC traffic
@@ -198,20 +204,25 @@ def main():
     o_ptr = [obs_buf[t].data_ptr() for t in range(T)]
     r_ptr = [rew_buf[t].data_ptr() for t in range(T)]
 
-    # HIP events on the kernel's own stream bracket the run of consecutive step launches t = 1..T-1 of
-    # every timed episode (no reset inside): per-launch duration = elapsed / (T - 1), back-to-back
-    # dispatch gaps included. One pair per episode: a pair per step would cost ~7 us of GPU time
-    # each and slow the very loop being measured (tools/launch_probe.py).
-    def run(steps, events=None):
+    # HIP events on the kernel's own stream bracket every run of consecutive step launches between two
+    # resets (at most one episode, and the part of one that the timed region holds): per-launch
+    # duration = elapsed / launches of the run, back-to-back dispatch gaps included, the reset kernel
+    # outside every pair. Every timed step launch lies in exactly one pair, whatever K and W are. One
+    # pair per episode: a pair per step would cost ~7 us of GPU time each and slow the very loop
+    # being measured (tools/launch_probe.py).
+    def run(first, steps, events=None):
+        """Steps first .. first+steps-1 of the bench's step sequence (period t = step mod T)."""
         pair = None
-        for s in range(steps):
+        for s in range(first, first + steps):
             t = s % T
             if t == 0:
                 nat.check(lib.imenv_reset(h, None, nat.LAYOUT_DRAW, 0, 0.0, None, -1, obs0.data_ptr(), nat.F32,
                                           sptr), "imenv_reset")
-            if events is not None and t == 1 and s + T - 1 <= steps:
-                pair = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            if events is not None and pair is None:
+                pair = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), []]
                 pair[0].record(stream)
+            if pair is not None:
+                pair[2].append(t)
             if gather is None:
                 rc = lib.imenv_step(h, a_ptr[t], nat.F32, o_ptr[t], nat.F32, r_ptr[t], None, None, sptr)
             else:
@@ -221,34 +232,40 @@ def main():
                                     gather.reward_out(s).data_ptr(), None, None, sptr)
             if rc:
                 nat.check(rc, "imenv_step")
-            if pair is not None and t == T - 1:
+            if pair is not None and (t == T - 1 or s == first + steps - 1):
                 pair[1].record(stream)
                 events.append(pair)
                 pair = None
             if gather is not None:
                 gather.start(s)
-                if s >= 1:
+                if s > first:
                     gather.result(s - 1)     # the learner's view of step s-1: [world*n, N, F], [world*n]
         if gather is not None and steps:
-            gather.result(steps - 1)
+            gather.result(first + steps - 1)
 
-    # warmup (whole episodes so the timed region starts at a reset)
-    w = ((args.warmup + T - 1) // T) * T
-    run(w)
+    # exactly W untimed warmup steps (the first one resets); the timed region continues the same step
+    # sequence, so it holds whatever resets fall at its episode boundaries
+    W, K = args.warmup, args.steps
+    run(0, W)
     torch.cuda.synchronize(dev)
-    K = args.steps
     events = []
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    run(K, events)
+    run(W, K, events)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) / (T - 1)
+    # per-launch kernel time and the algorithmic bytes of exactly the launches that were timed
+    per_t = env.step_traffic_per_period()
+    kern_sum_ms = sum(a.elapsed_time(b) for a, b, _ in events)
+    launches = sum(len(ts) for _, _, ts in events)
+    timed_bytes = sum(per_t[t] for _, _, ts in events for t in ts) * n
+    kern_ms = kern_sum_ms / launches
+    bytes_per_launch = timed_bytes / launches
 
     if world > 1:
         tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
@@ -275,7 +292,7 @@ def main():
     total_env_steps = world * n * K
     value = total_env_steps / el
     es = env.state_layout()[0]
-    achieved_gbs = (b_avg * n) / (kern_ms * 1e-3) / 1e9
+    achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic = pmc_traffic(n, env.kernel_info())
     out = {
         "metric": METRIC,
@@ -283,7 +300,7 @@ def main():
         "unit": "env-steps/s",
         "n_gpus": world,
         "steps": K,
-        "warmup": w,
+        "warmup": W,
         "ms_per_step": round(el / K * 1e3, 6),
         "higher_is_better": True,
         "scaling": "weak",
@@ -308,10 +325,11 @@ def main():
             "copy_ceiling_gbs": round(copy_gbs, 1),
             "kernel": env.kernel_info(),
             "kernel_us": round(kern_ms * 1e3, 3),
-            "kernel_samples": len(events) * (T - 1),
-            "bytes_per_env_step": round(b_avg, 3),
+            "kernel_samples": launches,
+            "bytes_per_env_step": round(bytes_per_launch / n, 3),
             "bytes_per_env_step_steady": b_steady,
-            "bytes_per_launch": round(b_avg * n),
+            "bytes_per_env_step_episode_avg": round(b_avg, 3),
+            "bytes_per_launch": round(bytes_per_launch),
         },
         "cpu_baseline": cpu,
     }

@@ -262,7 +262,12 @@ class VectorInvEnv:
         return eb.value, rl.value, rd.value
 
     def step_traffic(self, action_bytes=4, obs_bytes=4, host_demand=False, metrics=False):
-        """Algorithmic HBM bytes of one step() per env: (steady state, average over an episode).
+        """Algorithmic HBM bytes of one step() per env: (steady state, average over an episode)."""
+        per = self.step_traffic_per_period(action_bytes, obs_bytes, host_demand, metrics)
+        return per[-1], float(np.mean(per))
+
+    def step_traffic_per_period(self, action_bytes=4, obs_bytes=4, host_demand=False, metrics=False):
+        """Algorithmic HBM bytes of the step() at period t per env, for t = 0 .. T-1.
 
         The minimal traffic of this handle's layout: actions; the net-inventory
         (inv - backlog) and order_u rows read + written (no read at t = 0: the initial state is
@@ -303,7 +308,7 @@ class VectorInvEnv:
             if metrics:
                 b += 16 * (4 + N) - (8 * (4 + N) if t == 0 else 0)
             per.append(b)
-        return per[-1], float(np.mean(per))
+        return per
 
     def set_jit(self, mode):
         """1: hipRTC kernel specialised for this spec (default); 0: ahead-of-time kernels."""
