@@ -181,6 +181,11 @@ __global__ void __launch_bounds__(256) imenv_colsum_finalize_kernel(const double
 //   [ clip(action[o], lo, hi) for o != m ][ obs[o][:] for o != m ][ obs[m][:] ]
 // (o in agent order). One thread per output element: the writes are one contiguous stream, the
 // reads gather from the env's own [N][F] obs row and [N] action row (cache-resident).
+// np.clip (models/CC_Model.py:165-193; oracle/cc_obs.py:20): NaN passes through (fmin/fmax alone would turn it into lo)
+__device__ __forceinline__ double np_clip(double x, double lo, double hi) {
+  return x != x ? x : fmin(fmax(x, lo), hi);
+}
+
 template <typename OT, typename AT>
 __global__ void __launch_bounds__(256) imenv_cc_obs_kernel(const OT* __restrict__ obs, const AT* __restrict__ act,
                                                            int64_t n, int N, int F, double lo, double hi,
@@ -197,7 +202,7 @@ __global__ void __launch_bounds__(256) imenv_cc_obs_kernel(const OT* __restrict_
     OT v;
     if (j < N - 1) {                          // opponent_action
       const int o = j < m ? j : j + 1;
-      v = act ? (OT)fmin(fmax((double)act[e * N + o], lo), hi) : (OT)0;
+      v = act ? (OT)np_clip((double)act[e * N + o], lo, hi) : (OT)0;
     } else if (j < (N - 1) * (F + 1)) {       // opponent_obs
       const int k = j - (N - 1);
       const int oi = k / F;
@@ -230,7 +235,7 @@ __global__ void __launch_bounds__(BS) imenv_cc_obs_slab_kernel(const OT* __restr
   OT* s_out = s_obs + E * N * F;                                          // [E * N][WP]
   for (int q = tid; q < ne * N * F; q += BS) s_obs[q] = obs[e0 * N * F + q];
   for (int q = tid; q < ne * N; q += BS)
-    s_act[q] = act ? fmin(fmax((double)act[e0 * N + q], lo), hi) : 0.0;
+    s_act[q] = act ? np_clip((double)act[e0 * N + q], lo, hi) : 0.0;
   __syncthreads();
   if (tid < ne * N) {
     const int el = tid / N, m = tid - el * N;
@@ -842,11 +847,13 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
         } else {
           h->jit_err = msg;
           if (h->jit_strict) return fail(IMENV_E_UNSUPPORTED, "JIT step kernel: " + msg);
-          h->jit = 0;   // recorded in imenv_kernel_info; the ahead-of-time kernels take over
+          // recorded in imenv_kernel_info; the ahead-of-time kernels take over for THIS flag set only
+          // (an empty entry: no retry per step), other flag sets of the handle keep their JIT kernels
+          it = h->jit_k.emplace(f.key(), imenv::JitKernel{}).first;
         }
       }
     }
-    if (it != h->jit_k.end()) {
+    if (it != h->jit_k.end() && it->second.fn) {
       HIPCHK(imenv::jit_launch(it->second, st, h->d_spec, A));
       h->last_kernel = it->second.tag;
       h->t += 1;
@@ -1176,7 +1183,10 @@ int imenv_set_jit(ImEnv* h, int mode) {
   if (mode != 0 && mode != 1) return fail(IMENV_E_INVALID, "mode must be 0 (ahead-of-time) or 1 (hipRTC)");
   if (mode == 1 && h->arch.empty()) return fail(IMENV_E_UNSUPPORTED, "device architecture unknown");
   h->jit = mode;
-  if (mode == 1) h->jit_err.clear();
+  if (mode == 1) {   // retry flag sets whose compile failed
+    h->jit_err.clear();
+    for (auto it = h->jit_k.begin(); it != h->jit_k.end();) it = it->second.fn ? std::next(it) : h->jit_k.erase(it);
+  }
   return IMENV_OK;
 }
 

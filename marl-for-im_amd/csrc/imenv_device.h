@@ -1219,7 +1219,8 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           const int total = cnt * row;
           double* gobs = static_cast<double*>(A.obs) + e0 * row;
           const double* so = reinterpret_cast<const double*>(s_obs + k * SLAB);
-          if ((total & 1) == 0) {
+          // 16-byte stores need a 16-byte aligned destination (a caller's obs_out view may be offset)
+          if ((total & 1) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0) {
             double2* g2 = reinterpret_cast<double2*>(gobs);
             for (int q = tid; q < total / 2; q += BS) g2[q] = make_double2(at(so, 2 * q), at(so, 2 * q + 1));
           } else {
@@ -1242,7 +1243,7 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           const int total = cnt * row;
           float* gobs = static_cast<float*>(A.obs) + e0 * row;
           const float* so = s_obs + k * SLAB;
-          if ((total & 3) == 0) {
+          if ((total & 3) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0) {
             float4* g4 = reinterpret_cast<float4*>(gobs);
             if constexpr (SSTR == row) {
               const float4* s4 = reinterpret_cast<const float4*>(so);

@@ -67,26 +67,36 @@ int jit_block_size() {
   return bs;
 }
 
-// General observation rows (not the base [N][3] layout) are staged in LDS when a block's slab fits
-// kStageLds bytes: the block size halves (256 -> 128 -> 64, unless IMENV_JIT_BS is set) until it does,
-// so wide rows (8 stages with in-transit features, 2-level trees with shared-network ids) keep
-// coalesced float4 stores at 4+ waves per SIMD instead of falling back to strided scalar stores.
-// vbytes: 4 (float32 observations) or 8 (float64, staged as doubles).
+// Observation rows are staged in LDS when a block's slab fits kStageLds bytes. The base [N][3] row
+// (N <= 8) is always staged, so the block size halves (down to 64) until its slab fits, also under
+// IMENV_JIT_BS: a slab over the static LDS limit would fail the hipRTC compile. General rows: the
+// block size halves (256 -> 128 -> 64, unless IMENV_JIT_BS is set) until the slab fits, so wide rows
+// (8 stages with in-transit features, 2-level trees with shared-network ids) keep coalesced float4
+// stores at 4+ waves per SIMD instead of falling back to strided scalar stores; a general row that
+// still does not fit is stored directly (jit_obs_row = 0).
+// vbytes: 4 (float32 observations) or 8 (float64, staged as doubles); ept: envs per thread.
 constexpr int kStageLds = 48 * 1024;
 
 int general_row(const SpecDev& d, bool base) { return base ? 0 : d.s.num_nodes * d.s.num_features; }
+// the row the step kernel stages (imenv_device.h stage_row) and its padded LDS stride (stage_stride)
+int staged_row(const SpecDev& d, bool base) {
+  return base ? (d.s.num_nodes <= 8 ? 3 * d.s.num_nodes : 0) : general_row(d, base);
+}
+int staged_stride(int row, int vbytes) { return (row > 0 && row % (vbytes == 8 ? 2 : 8) == 0) ? row + 1 : row; }
+int64_t slab_bytes(const SpecDev& d, bool base, int bs, int vbytes, int ept) {
+  return (int64_t)bs * ept * staged_stride(staged_row(d, base), vbytes) * vbytes;
+}
 
-int jit_step_block_size(const SpecDev& d, bool base, int vbytes) {
+int jit_step_block_size(const SpecDev& d, bool base, int vbytes, int ept) {
   int bs = jit_block_size();
-  const int row = general_row(d, base);
-  if (row > 0 && !std::getenv("IMENV_JIT_BS"))
-    while (bs > 64 && bs * row * vbytes > kStageLds) bs /= 2;
+  if (staged_row(d, base) > 0 && (base || !std::getenv("IMENV_JIT_BS")))
+    while (bs > 64 && slab_bytes(d, base, bs, vbytes, ept) > kStageLds) bs /= 2;
   return bs;
 }
 
 int jit_obs_row(const SpecDev& d, bool base, int bs, int vbytes) {
   const int row = general_row(d, base);
-  return (row > 0 && bs * row * vbytes <= kStageLds) ? row : 0;
+  return (row > 0 && slab_bytes(d, base, bs, vbytes, 1) <= kStageLds) ? row : 0;
 }
 
 // Envs per thread of the JIT step kernel (step_body). 1: with two envs per thread the footprint probe
@@ -294,8 +304,8 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
 
 std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f) {
   std::ostringstream o;
-  emit_policy(o, d, maxc, base, f, jit_step_block_size(d, base, f.obs_f64 ? 8 : 4),
-              jit_envs_per_thread(d, base, f.obs_f64));
+  const int ept = jit_envs_per_thread(d, base, f.obs_f64);
+  emit_policy(o, d, maxc, base, f, jit_step_block_size(d, base, f.obs_f64 ? 8 : 4, ept), ept);
   o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
        "imenv_step_jit(const imenv::SpecDev* __restrict__ sp, const imenv::StepArgs A) {\n"
        "  __shared__ uint32_t s_tab[JitSpec::TAB_LDS];\n"
@@ -408,8 +418,8 @@ bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const st
               std::string& msg) {
   const std::string src = jit_source(d, maxc, base, f);
   if (!load_module(src, arch, "imenv_step_jit", out, msg)) return false;
-  out.bs = jit_step_block_size(d, base, f.obs_f64 ? 8 : 4);
   out.ept = jit_envs_per_thread(d, base, f.obs_f64);
+  out.bs = jit_step_block_size(d, base, f.obs_f64 ? 8 : 4, out.ept);
   char tag[160];
   // dev=: hash of the device-code header, so a profile of an older kernel body never matches this one
   std::snprintf(tag, sizeof tag, "jit:imenv_step_jit[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,ept=%d,%zuB,dev=%08x]",

@@ -62,17 +62,25 @@ def test_gpu_cc_observation_rollout_buffer():
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,F", [(2, 1), (3, 3), (4, 3), (5, 2), (8, 7), (16, 4), (16, 12)])
 @pytest.mark.parametrize("dt", ["f32", "f64"])
-def test_gpu_cc_observation_shapes(N, F, dt):
+@pytest.mark.parametrize("bs", ["256", "512"])
+def test_gpu_cc_observation_shapes(N, F, dt, bs, monkeypatch):
     """Staged (env, agent)-row kernel (blocks of 256 // N envs: ragged when N does not divide 256, odd
-    and even row lengths) and, for rows too wide for its 48 KiB slab (16 agents x 12 features), the
-    element-wise kernel; env counts that leave a partial last block. Bit-exact vs the oracle."""
+    and even row lengths; IMENV_CC_BS=512 runs the 512-thread variant, read on every call) and, for
+    rows too wide for its 48 KiB slab (16 agents x 12 features), the element-wise kernel; env counts
+    that leave a partial last block. NaN and infinite actions clip as np.clip does (NaN passes
+    through). Bit-exact vs the oracle."""
     import torch
     from imenv.critic import cc_observation
+    monkeypatch.setenv("IMENV_CC_BS", bs)
     tdt = {"f32": torch.float32, "f64": torch.float64}[dt]
     g = torch.Generator(device="cuda:0")
     g.manual_seed(N * 100 + F)
     for n in (1, 7, 1000, 4099):
         obs = (torch.rand((n, N, F), generator=g, device="cuda:0", dtype=torch.float64) * 4 - 2).to(tdt)
         act = (torch.rand((n, N), generator=g, device="cuda:0", dtype=torch.float64) * 3 - 1.5).to(tdt)
+        if n >= 7:
+            act.view(-1)[[1, 5]] = float("nan")
+            act.view(-1)[2] = float("inf")
+            act.view(-1)[3] = -float("inf")
         got = cc_observation(obs, act).cpu().numpy()
         np.testing.assert_array_equal(got, cc_ref(obs.cpu().numpy(), act.cpu().numpy()), err_msg="n=%d" % n)

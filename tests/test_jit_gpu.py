@@ -1,0 +1,117 @@
+"""hipRTC step-kernel selection: the observation slab stays within its LDS budget under any
+IMENV_JIT_BS, and a compile failure sends only its own flag set to the ahead-of-time kernels (the
+other flag sets of the handle keep their specialised kernels). Results bit-exact vs the reference's
+golden vectors either way."""
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from golden_io import load_case
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+STAGE_LDS = 48 * 1024      # kStageLds, imenv_jit.hip
+
+
+def _episode(env, meta, d, obs_dtype):
+    serial = meta["kind"] in ("IM", "MAIM")
+    dem = d["customer_demand"]
+    env.reset(customer_demand=dem[:, 0, :] if serial else dem)
+    obs, rew = [], []
+    for t in range(meta["T"]):
+        a = torch.as_tensor(d["actions"][:, t, :], dtype=torch.float64, device=DEV)
+        o, r, _, _ = env.step(a)
+        obs.append(o.cpu().numpy())
+        r = r.cpu().numpy()
+        rew.append(r if r.ndim == 2 else r[:, None])
+    exp = d["obs"] if obs_dtype == torch.float64 else d["obs"].astype(np.float32)
+    np.testing.assert_array_equal(np.stack(obs, axis=1), exp)
+    ref_r = d["reward"]
+    got_r = np.stack(rew, axis=1)
+    np.testing.assert_array_equal(got_r, ref_r[..., :got_r.shape[-1]])
+
+
+@pytest.mark.parametrize("name", ["C3_IM8", "IM8_td", "MAIM_div2_share", "C2_MAIM4"])
+@pytest.mark.parametrize("odt", ["f32", "f64"])
+def test_gpu_jit_block_size_bounds_the_obs_slab(name, odt, monkeypatch):
+    """IMENV_JIT_BS=1024: an 8-stage base row staged as float64 would need 1024 x 25 x 8 B = 200 KiB of
+    LDS (over the static limit, so the hipRTC compile failed and the handle lost its JIT kernels);
+    the block size now halves until the staged slab fits, for base rows as for general ones."""
+    from imenv import VectorInvEnv
+    monkeypatch.setenv("IMENV_JIT_BS", "1024")
+    monkeypatch.setenv("IMENV_JIT_STRICT", "1")
+    meta, d = load_case(name)
+    tdt = torch.float64 if odt == "f64" else torch.float32
+    env = VectorInvEnv(meta["kind"], meta["config"], n_envs=meta["E"], device=DEV, obs_dtype=tdt)
+    _episode(env, meta, d, tdt)
+    info = env.kernel_info()
+    assert info.startswith("jit:") and "jit failed" not in info, info
+    bs = int(re.search(r"bs=(\d+)", info).group(1))
+    N, F = d["obs"].shape[2], d["obs"].shape[3]
+    vb = 8 if odt == "f64" else 4
+    base = "base=1" in info
+    row = 3 * N if base else N * F
+    stride = row + 1 if row % (2 if vb == 8 else 8) == 0 else row
+    if base:
+        assert bs * stride * vb <= STAGE_LDS, (bs, stride, vb)
+    env.close()
+
+
+def test_gpu_jit_failure_falls_back_for_its_flag_set_only(monkeypatch):
+    """A flag set whose hipRTC compile fails (forced here by pre-including a header that does not exist) runs on the
+    ahead-of-time kernel, bit-exact; the handle's next flag set (float64 observations) still gets
+    its JIT kernel, and set_jit(1) retries the failed one."""
+    from imenv import VectorInvEnv
+    monkeypatch.setenv("IMENV_JIT_STRICT", "0")
+    meta, d = load_case("C2_MAIM4")
+    env = VectorInvEnv(meta["kind"], meta["config"], n_envs=meta["E"], device=DEV, obs_dtype=torch.float32)
+    monkeypatch.setenv("IMENV_JIT_OPTS", "-include imenv_no_such_header_probe.h")
+    _episode(env, meta, d, torch.float32)
+    info = env.kernel_info()
+    assert info.startswith("aot:") and "jit failed" in info, info
+    monkeypatch.delenv("IMENV_JIT_OPTS")
+    env.obs_dtype = torch.float64
+    _episode(env, meta, d, torch.float64)
+    assert env.kernel_info().startswith("jit:"), env.kernel_info()
+    env.obs_dtype = torch.float32
+    _episode(env, meta, d, torch.float32)
+    assert env.kernel_info().startswith("aot:")     # the failed flag set stays on AOT ...
+    env.set_jit(1)
+    _episode(env, meta, d, torch.float32)
+    assert env.kernel_info().startswith("jit:"), env.kernel_info()   # ... until set_jit(1) retries it
+    env.close()
+
+
+@pytest.mark.parametrize("name", ["C2_MAIM4", "C3_IM8", "MAIM_div2_share"])
+@pytest.mark.parametrize("odt", ["f32", "f64"])
+@pytest.mark.parametrize("mode", [1, 0])
+def test_gpu_misaligned_obs_out_view(name, odt, mode):
+    """A caller-owned obs_out that is a view one element into a larger buffer (8-byte aligned for
+    float64, 4-byte for float32, never 16): the staged slab write-out drops to element stores and the
+    observations equal those written into an aligned buffer."""
+    from imenv import VectorInvEnv
+    meta, d = load_case(name)
+    tdt = torch.float64 if odt == "f64" else torch.float32
+    serial = meta["kind"] in ("IM", "MAIM")
+    dem = d["customer_demand"]
+    envs = []
+    for _ in range(2):
+        e = VectorInvEnv(meta["kind"], meta["config"], n_envs=meta["E"], device=DEV, obs_dtype=tdt)
+        e.set_jit(mode)
+        e.reset(customer_demand=dem[:, 0, :] if serial else dem)
+        envs.append(e)
+    n, N, F = meta["E"], d["obs"].shape[2], d["obs"].shape[3]
+    big = torch.empty(n * N * F + 1, dtype=tdt, device=DEV)
+    view = big[1:].view(n, N, F)
+    assert view.data_ptr() % 16 != 0
+    for t in range(meta["T"]):
+        a = torch.as_tensor(d["actions"][:, t, :], dtype=torch.float64, device=DEV)
+        ref, _, _, _ = envs[0].step(a)
+        envs[1].step(a, obs_out=view)
+        np.testing.assert_array_equal(view.cpu().numpy(), ref.cpu().numpy(), err_msg="t=%d" % t)
+    exp = d["obs"][:, -1] if tdt == torch.float64 else d["obs"][:, -1].astype(np.float32)
+    np.testing.assert_array_equal(view.cpu().numpy(), exp)
+    for e in envs:
+        e.close()
