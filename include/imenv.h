@@ -333,8 +333,9 @@ int imenv_set_delay_uniforms(ImEnv* env, int32_t period, const double* u, void* 
  * default): step() runs a kernel compiled at run time with hipRTC for this spec, every spec value
  * a compile-time constant (first step per dtype/layout combination pays ~1 s of compilation;
  * cached per process). mode 0: the ahead-of-time kernels, which read the spec from device memory.
- * Both compute the same function; a JIT failure falls back to mode 0 and is reported by
- * imenv_kernel_info (IMENV_JIT_STRICT=1 turns it into an IMENV_E_UNSUPPORTED from step()). */
+ * Both compute the same function; a JIT failure sends that dtype/layout combination (only) to the
+ * mode-0 kernels and is reported by imenv_kernel_info (IMENV_JIT_STRICT=1 turns it into an
+ * IMENV_E_UNSUPPORTED from step()); set_jit(1) retries failed combinations. */
 int imenv_set_jit(ImEnv* env, int mode);
 
 /* NUL-terminated description of the kernel the last step() launched, truncated to len bytes. */
