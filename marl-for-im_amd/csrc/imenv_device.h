@@ -50,6 +50,9 @@ typedef unsigned long long uint64_t;
 #include "imenv.h"
 
 #define IMENV_TABLE_MAX 1024
+#ifndef IMENV_WAVE_SLAB
+#define IMENV_WAVE_SLAB 0    // 1: each wave writes out its own staged observation rows (step_body)
+#endif
 #define IMENV_GUIDE_BITS 10
 
 namespace imenv {
@@ -1189,7 +1192,6 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
 // contiguous float4 runs after one barrier.
 template <class P>
 __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_t* s_tab, float* s_obs) {
-  constexpr int NT = P::NT;
   constexpr int BS = P::BS;
   constexpr int EPT = P::EPT;
   constexpr int SROW = stage_row<P>();   // LDS floats per env (0: observations stored directly)
@@ -1205,26 +1207,41 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   constexpr int SLAB = BS * SSTR * (P::OBS_STAGE64 ? 2 : 1);   // floats per BS-env slab
 #pragma unroll
   for (int k = 0; k < EPT; ++k) step_finish(p, A, eb + k * BS + tid, L[k], s_tab, s_obs + k * SLAB);
+  // Write-out group: the block (one barrier), or with IMENV_WAVE_SLAB each wave on its own (the 64 rows
+  // it staged itself: LDS ops of one wave complete in order, so a wavefront fence replaces the block
+  // barrier and no wave waits for its block's slowest wave)
+  constexpr int GS = IMENV_WAVE_SLAB ? 64 : BS;
+  [[maybe_unused]] const int gl = tid % GS, gi = tid / GS;
+  if constexpr (SROW > 0) {
+    if (staged_obs(p)) {
+      if constexpr (IMENV_WAVE_SLAB) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else {
+        __syncthreads();
+      }
+    }
+  }
   if constexpr (SROW > 0 && P::OBS_STAGE64) {
     // float64 rows: the same write-out in 16-byte double2 runs
     if (staged_obs(p)) {
-      __syncthreads();
       constexpr int row = SROW;
       auto at = [](const double* so, int q) { return so[(q / row) * SSTR + q % row]; };
 #pragma unroll
       for (int k = 0; k < EPT; ++k) {
-        const int64_t e0 = eb + k * BS;
+        const int64_t e0 = eb + k * BS + gi * GS;
         if (e0 < n) {
-          const int cnt = (n - e0) < BS ? (int)(n - e0) : BS;
+          const int cnt = (n - e0) < GS ? (int)(n - e0) : GS;
           const int total = cnt * row;
           double* gobs = static_cast<double*>(A.obs) + e0 * row;
-          const double* so = reinterpret_cast<const double*>(s_obs + k * SLAB);
+          const double* so = reinterpret_cast<const double*>(s_obs + k * SLAB) + gi * GS * SSTR;
           // 16-byte stores need a 16-byte aligned destination (a caller's obs_out view may be offset)
           if ((total & 1) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0) {
             double2* g2 = reinterpret_cast<double2*>(gobs);
-            for (int q = tid; q < total / 2; q += BS) g2[q] = make_double2(at(so, 2 * q), at(so, 2 * q + 1));
+            for (int q = gl; q < total / 2; q += GS) g2[q] = make_double2(at(so, 2 * q), at(so, 2 * q + 1));
           } else {
-            for (int q = tid; q < total; q += BS) gobs[q] = at(so, q);
+            for (int q = gl; q < total; q += GS) gobs[q] = at(so, q);
           }
         }
       }
@@ -1232,28 +1249,27 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   } else if constexpr (SROW > 0) {
     // (staged rows: SROW == 3 N for the base layout, as N == NT whenever it is staged)
     if (staged_obs(p)) {
-      __syncthreads();
       constexpr int row = SROW;
       auto at = [](const float* so, int q) { return so[(q / row) * SSTR + q % row]; };   // packed -> slab
 #pragma unroll
       for (int k = 0; k < EPT; ++k) {
-        const int64_t e0 = eb + k * BS;
+        const int64_t e0 = eb + k * BS + gi * GS;
         if (e0 < n) {
-          const int cnt = (n - e0) < BS ? (int)(n - e0) : BS;
+          const int cnt = (n - e0) < GS ? (int)(n - e0) : GS;
           const int total = cnt * row;
           float* gobs = static_cast<float*>(A.obs) + e0 * row;
-          const float* so = s_obs + k * SLAB;
+          const float* so = s_obs + k * SLAB + gi * GS * SSTR;
           if ((total & 3) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0) {
             float4* g4 = reinterpret_cast<float4*>(gobs);
             if constexpr (SSTR == row) {
               const float4* s4 = reinterpret_cast<const float4*>(so);
-              for (int q = tid; q < total / 4; q += BS) g4[q] = s4[q];
+              for (int q = gl; q < total / 4; q += GS) g4[q] = s4[q];
             } else {
-              for (int q = tid; q < total / 4; q += BS)
+              for (int q = gl; q < total / 4; q += GS)
                 g4[q] = make_float4(at(so, 4 * q), at(so, 4 * q + 1), at(so, 4 * q + 2), at(so, 4 * q + 3));
             }
           } else {
-            for (int q = tid; q < total; q += BS) gobs[q] = at(so, q);
+            for (int q = gl; q < total; q += GS) gobs[q] = at(so, q);
           }
         }
       }

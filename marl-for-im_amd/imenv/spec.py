@@ -273,7 +273,11 @@ def _serial(kind, cfg):
             mode[nat.G_DEMAND_HIST], den[nat.G_DEMAND_HIST] = nat.OBS_SCALED, imf
             mode[nat.G_ORDER_HIST], den[nat.G_ORDER_HIST] = nat.OBS_SCALED, omf
             mode[nat.G_TRANSIT], den[nat.G_TRANSIT] = nat.OBS_SCALED, imf
-            feats += _tail_feats(pd, pa, td, L, D)
+            if pd and not pa and not td:
+                # MAIM_env.py:296-317 has no branch for prev_demand alone: its L slots stay 0
+                feats += [(nat.G_ZERO, 0)] * L
+            else:
+                feats += _tail_feats(pd, pa, td, L, D)
         else:
             # MAIM_env.py:319-324: raw base; raw tds in slots 3..3+D-1; every other slot stays 0
             for gg in (nat.G_INV, nat.G_BACKLOG, nat.G_ORDER_U, nat.G_TRANSIT):

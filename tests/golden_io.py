@@ -28,6 +28,11 @@ def case_names():
     return sorted(n for n in names if n not in NON_CASE)
 
 
+def fuzz_case_names():
+    """Randomly drawn configurations (tools/gen_fuzz_fixtures.py), named "fuzz/<case>"."""
+    return sorted("fuzz/" + os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "fuzz", "*.npz")))
+
+
 def load_case(name):
     z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     d = {k: z[k] for k in z.files}

@@ -13,13 +13,14 @@ import numpy as np
 import pytest
 import torch
 
-from golden_io import case_names, load_case
+from golden_io import case_names, fuzz_case_names, load_case
 from oracle import philox
 from oracle.im_oracle import OracleEnv
 
 pytestmark = pytest.mark.gpu
 
 CASES = case_names()
+FUZZ = fuzz_case_names()     # randomly drawn configurations, reference outputs (tools/gen_fuzz_fixtures.py)
 DEV = "cuda:0"
 os.environ["IMENV_JIT_STRICT"] = "1"
 MODE = {"kernel": "jit"}
@@ -68,7 +69,7 @@ def run_gpu_case(meta, d, obs_dtype=torch.float64, action_dtype=torch.float64):
     return obs0, {k: np.stack(v, axis=1) for k, v in out.items()}, anyv
 
 
-@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("name", CASES + FUZZ)
 def test_gpu_matches_reference_golden(name):
     meta, d = load_case(name)
     obs0, out, anyerr = run_gpu_case(meta, d)
@@ -86,7 +87,7 @@ def test_gpu_matches_reference_golden(name):
 
 
 @pytest.mark.parametrize("name", ["C1_IM4", "C2_MAIM4", "C3_IM8", "C4_MAIM_div1", "MAIM_div2_share",
-                                  "IM4_td_pd_pa_L2"])
+                                  "IM4_td_pd_pa_L2", "fuzz/fz01_MAIM", "fuzz/fz04_IM", "fuzz/fz19_MAIM_div"])
 def test_gpu_float32_obs_is_rounded_reference(name):
     meta, d = load_case(name)
     obs0, out, _ = run_gpu_case(meta, d, obs_dtype=torch.float32)

@@ -8,10 +8,10 @@ Every comparison here is exact (integer state and float64 obs/rewards bit-equal)
 import numpy as np
 import pytest
 
-from golden_io import case_names, load_case, load_kat
+from golden_io import case_names, fuzz_case_names, load_case, load_kat
 from oracle.im_oracle import OracleEnv, OracleError, np_sum_order
 
-CASES = case_names()
+CASES = case_names() + fuzz_case_names()
 
 
 def run_oracle(meta, d):
@@ -72,12 +72,15 @@ def test_net_inventory_invariant(name):
     meta, d = load_case(name)
     assert d["inv"].min() >= 0 and d["backlog"].min() >= 0
     assert not np.any(d["inv"] * d["backlog"]), name
-    env = OracleEnv(meta["kind"], meta["config"], n_envs=64)
+    # the drawn configurations reach capacities of ~56,000, where the oracle's literal unit-by-unit
+    # split loop is slow: fewer fresh episodes for them (their fixtures are checked in full above)
+    n, eps = (8, 1) if name.startswith("fuzz/") else (64, 3)
+    env = OracleEnv(meta["kind"], meta["config"], n_envs=n)
     rs = np.random.RandomState(5)
-    for ep in range(3):
+    for ep in range(eps):
         env.reset(rng=dict(seed=7, episode=ep, env_offset=0, dist="poisson", mu=5))
         for t in range(env.num_periods):
-            env.step(rs.uniform(-1.2, 1.2, size=(64, env.N)))
+            env.step(rs.uniform(-1.2, 1.2, size=(n, env.N)))
             st = env.state_arrays()
             assert not np.any(st["inv"] * st["backlog"]), (name, ep, t)
 
