@@ -397,7 +397,11 @@ def _tree(kind, cfg):
         mode[nat.G_TRANSIT], den[nat.G_TRANSIT] = nat.OBS_CLAMP_SCALED, imf * 2
         clip[nat.G_TRANSIT] = imf * 2
         mode[nat.G_NODE_ID], den[nat.G_NODE_ID] = nat.OBS_SCALED, np.full(N, float(N))
-    feats += _tail_feats(pd, pa, td, L, D, share)
+    if ma and pd and not pa and not td:
+        # MAIM_div_env.py:413-432 has no branch for prev_demand alone: its L slots stay 0
+        feats += [(nat.G_ZERO, 0)] * L + ([(nat.G_NODE_ID, 0)] if share else [])
+    else:
+        feats += _tail_feats(pd, pa, td, L, D, share)
     R = len(retailers)
     dist, mu, lu, custom = _demand_params(g, R, T)
     # guard limits: IM_div x(4,2,2,2), MAIM_div x(2,1,1,1) of demand_max (IM_div_env.py:424-497)

@@ -66,7 +66,7 @@ def test_adaptor_reproduces_reference_session(name):
     def record(what, *args):
         if what == "reset":
             got["reset_obs"].append(_obs_array(args[0], ma))
-            got["reset_demand"].append(np.asarray(args[1], dtype=np.int64).reshape(-1))
+            got["reset_demand"].append(np.array(args[1], dtype=np.int64).reshape(-1))   # a copy
             return
         obs, r, d, info = args
         got["obs"].append(_obs_array(obs, ma))

@@ -383,6 +383,7 @@ def adaptor_script(env, kind, opts, rs, record):
 def adaptor_traces(classes):
     for name, (kind, cfg, opts) in ADAPTOR_CASES.items():
         ma = kind in ("MAIM", "MAIM_div")
+        meta_cfg = jsonable(cfg)    # before the session: the reference mutates a custom demand array in place
         caller = dict(cfg)
         env = classes[kind](caller)
         rec = {"reset_obs": [], "reset_demand": [], "obs": [], "reward": [], "done": [], "period": [],
@@ -392,7 +393,7 @@ def adaptor_traces(classes):
         def record(what, *args):
             if what == "reset":
                 rec["reset_obs"].append(obs_array(args[0], ma, N))
-                rec["reset_demand"].append(np.asarray(args[1], dtype=np.int64).reshape(-1))
+                rec["reset_demand"].append(np.array(args[1], dtype=np.int64).reshape(-1))   # a copy
                 return
             obs, r, d, info = args
             rec["obs"].append(obs_array(obs, ma, N))
@@ -416,7 +417,7 @@ def adaptor_traces(classes):
         adaptor_script(env, kind, opts, np.random.RandomState(7), record)
         out = {k: np.array(v) for k, v in rec.items() if k != "reset_demand"}
         out["reset_demand"] = np.array(rec["reset_demand"])
-        out["meta"] = json.dumps(dict(kind=kind, config=jsonable(cfg), opts=opts,
+        out["meta"] = json.dumps(dict(kind=kind, config=meta_cfg, opts=opts,
                                       caller_keys_after=sorted(caller.keys())))
         os.makedirs(os.path.join(OUT, "adaptor"), exist_ok=True)
         np.savez_compressed(os.path.join(OUT, "adaptor", name + ".npz"), **out)
