@@ -52,7 +52,12 @@ def test_rollout_matches_reference_golden(name):
     ro.close()
 
 
-@pytest.mark.parametrize("name", [c for c in ROLL if META[c]["kind"] in ("IM_div", "MAIM_div")])
+def _retailers(cfg):
+    return sum(1 for v in cfg["connections"].values() if not v)
+
+
+@pytest.mark.parametrize("name", [c for c in ROLL if META[c]["kind"] in ("IM_div", "MAIM_div")
+                                  and _retailers(META[c]["config"]) > 1])
 @pytest.mark.parametrize("replay", ["0", "1"])
 def test_tree_objective_single_pass_and_replay(name, replay, monkeypatch):
     """Trees (R > 1 retailer rows): the single-pass kernel parks rows 1..R-1 of the objective's terms

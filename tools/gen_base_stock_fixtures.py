@@ -37,10 +37,37 @@ CASES = {
 }
 
 
-def policies_for(N, P, rs):
+def fuzz_cases(num=8):
+    """Drawn single-agent configurations (tests/fuzz_configs.py) for dfo_func: IM and IM_div, raw or
+    standardised actions, Poisson or uniform demand at the capacity's scale, the objective's
+    retailer rows x periods within the kernel's pairwise-sum block (R * T <= 128)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+    from fuzz_configs import maybe_order_max, rand_config
+    rs = np.random.RandomState(31337)
+    out = {}
+    for i in range(num):
+        kind = ("IM", "IM_div")[i % 2]
+        while True:
+            cfg = maybe_order_max(rs, kind, rand_config(rs, kind, (i // 2) % 4))
+            R = sum(1 for v in cfg["connections"].values() if not v) if kind == "IM_div" else 1
+            if R * cfg["num_periods"] <= 128:
+                break
+        top = float(np.max(cfg["inv_max"]))
+        if i % 3 == 2:
+            lo = int(rs.randint(0, max(2, int(top // 4))))
+            cfg.update(demand_dist="uniform", lower_upper=(lo, lo + 2 + int(rs.randint(0, max(2, int(top // 2))))))
+            mu = None
+        else:
+            mu = float(np.round(rs.uniform(0.05, 0.5) * top, 1))
+            cfg.update(demand_dist="poisson", mu=mu)
+        out["fz%d_%s" % (i, kind)] = (kind, cfg, 3, 4, mu)
+    return out
+
+
+def policies_for(N, P, rs, top=60.0):
     pol = [np.ones(N) * 25.0, np.arange(1, N + 1) * 10.0]
     while len(pol) < P:
-        pol.append(rs.uniform(0.0, 60.0, size=N))     # non-integral levels, some above capacity
+        pol.append(rs.uniform(0.0, top, size=N))      # non-integral levels, some above capacity
     return np.array(pol[:P])
 
 
@@ -53,7 +80,7 @@ def main():
 
     out = {}
     meta = {}
-    for ci, (name, (kind, cfg, P, S, mu)) in enumerate(CASES.items()):
+    for ci, (name, (kind, cfg, P, S, mu)) in enumerate(list(CASES.items()) + list(fuzz_cases().items())):
         rs = np.random.RandomState(420 + ci)
         env = classes[kind](dict(cfg))
         N = env.num_nodes if hasattr(env, "num_nodes") else env.num_stages
@@ -65,7 +92,7 @@ def main():
         else:
             dem = rs.poisson(mu, size=(S, R, T))
         dem = dem[:, 0, :] if kind == "IM" else dem
-        pol = policies_for(N, P, rs)
+        pol = policies_for(N, P, rs, 60.0 if not name.startswith("fz") else 1.5 * float(np.max(cfg["inv_max"])))
         obj = np.zeros((P, S))
         rew = np.zeros((P, S, T))
         ret = np.zeros((P, S))
