@@ -219,7 +219,7 @@ def main():
                 nat.check(lib.imenv_reset(h, None, nat.LAYOUT_DRAW, 0, 0.0, None, -1, obs0.data_ptr(), nat.F32,
                                           sptr), "imenv_reset")
             if events is not None and pair is None:
-                pair = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), []]
+                pair = [pool.pop(), pool.pop(), []]
                 pair[0].record(stream)
             if pair is not None:
                 pair[2].append(t)
@@ -247,6 +247,11 @@ def main():
     # sequence, so it holds whatever resets fall at its episode boundaries
     W, K = args.warmup, args.steps
     run(0, W)
+    # the timed region's event pairs, created (and their HIP events allocated by one record each)
+    # before it starts: one pair per run of steps between resets
+    pool = [torch.cuda.Event(enable_timing=True) for _ in range(2 * (K // T + 2))]
+    for e in pool:
+        e.record(stream)
     torch.cuda.synchronize(dev)
     events = []
 
