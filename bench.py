@@ -150,6 +150,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--gather", action="store_true", help="add the per-step RCCL all-gather of obs+reward")
+    ap.add_argument("--store", default="default", choices=["default", "stream"],
+                    help="observation / reward store policy of the step kernel (imenv_set_store_policy)")
+    ap.add_argument("--no-alt-store", action="store_true", help="skip the informational run of the other policy")
     ap.add_argument("--cpu-only", action="store_true", help=argparse.SUPPRESS)
     # rehearsal of the multi-rank path on a one-GPU box: every rank on device 0, gloo for the
     # barrier / max-reduction (the driver's N-GPU runs use one GPU per rank and RCCL)
@@ -219,7 +222,7 @@ def main():
                 nat.check(lib.imenv_reset(h, None, nat.LAYOUT_DRAW, 0, 0.0, None, -1, obs0.data_ptr(), nat.F32,
                                           sptr), "imenv_reset")
             if events is not None and pair is None:
-                pair = [pool.pop(), pool.pop(), []]
+                pair = [pool.pop(), pool.pop(), []]     # pre-created in timed()
                 pair[0].record(stream)
             if pair is not None:
                 pair[2].append(t)
@@ -243,39 +246,54 @@ def main():
         if gather is not None and steps:
             gather.result(first + steps - 1)
 
-    # exactly W untimed warmup steps (the first one resets); the timed region continues the same step
-    # sequence, so it holds whatever resets fall at its episode boundaries
-    W, K = args.warmup, args.steps
-    run(0, W)
-    # the timed region's event pairs, created (and their HIP events allocated by one record each)
-    # before it starts: one pair per run of steps between resets
-    pool = [torch.cuda.Event(enable_timing=True) for _ in range(2 * (K // T + 2))]
-    for e in pool:
-        e.record(stream)
-    torch.cuda.synchronize(dev)
-    events = []
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    run(W, K, events)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    # per-launch kernel time and the algorithmic bytes of exactly the launches that were timed
     per_t = env.step_traffic_per_period()
-    kern_sum_ms = sum(a.elapsed_time(b) for a, b, _ in events)
-    launches = sum(len(ts) for _, _, ts in events)
-    timed_bytes = sum(per_t[t] for _, _, ts in events for t in ts) * n
-    kern_ms = kern_sum_ms / launches
-    bytes_per_launch = timed_bytes / launches
 
-    if world > 1:
-        tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el, kern_ms = tt[0].item(), tt[1].item()
+    def timed(W, K):
+        """W untimed warmup steps (the first one resets), then exactly K timed steps of the same step
+        sequence, so the timed region holds the resets at its episode boundaries. Returns (wall s,
+        kernel ms per launch, algorithmic bytes per timed launch), max over ranks."""
+        if W == 0:
+            run(0, 1)     # no warmup asked for: one step outside the sequence builds the hipRTC kernel
+        run(0, W)
+        # the timed region's event pairs, created (and their HIP events allocated by one record
+        # each) before it starts: one pair per run of steps between resets
+        pool[:] = [torch.cuda.Event(enable_timing=True) for _ in range(2 * (K // T + 2))]
+        for e in pool:
+            e.record(stream)
+        torch.cuda.synchronize(dev)
+        events = []
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        run(W, K, events)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        # per-launch kernel time and the algorithmic bytes of exactly the launches that were timed
+        kern_ms = sum(a.elapsed_time(b) for a, b, _ in events) / sum(len(ts) for _, _, ts in events)
+        bpl = sum(per_t[t] for _, _, ts in events for t in ts) * n / sum(len(ts) for _, _, ts in events)
+        if world > 1:
+            tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el, kern_ms = tt[0].item(), tt[1].item()
+        return el, kern_ms, bpl, sum(len(ts) for _, _, ts in events)
+
+    pool = []
+    W, K = args.warmup, args.steps
+    env.set_store_policy(args.store)
+    el, kern_ms, bytes_per_launch, launches = timed(W, K)
+    alt = None
+    if world == 1 and not args.no_alt_store:
+        # the other store policy on the same handle (informational; the line's value is args.store's)
+        other = "stream" if args.store == "default" else "default"
+        env.set_store_policy(other)
+        a_el, a_kern, a_bpl, _ = timed(W, K)
+        env.set_store_policy(args.store)
+        alt = {"store_policy": other, "value": round(n * K / a_el, 1), "ms_per_step": round(a_el / K * 1e3, 6),
+               "kernel_us": round(a_kern * 1e3, 3), "achieved": round(a_bpl / (a_kern * 1e-3) / 1e9, 1),
+               "frac": round(a_bpl / (a_kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
     # measured stream-copy ceiling at the step's byte count (SURVEY.md §8d): a device copy of half the
     # bytes moves them once in and once out; outside the timed region
@@ -335,6 +353,8 @@ def main():
             "bytes_per_env_step_steady": b_steady,
             "bytes_per_env_step_episode_avg": round(b_avg, 3),
             "bytes_per_launch": round(bytes_per_launch),
+            "store_policy": args.store,
+            "alt_store_policy": alt,
         },
         "cpu_baseline": cpu,
     }

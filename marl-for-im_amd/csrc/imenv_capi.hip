@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(256) imenv_cc_obs_kernel(const OT* __restrict_
 // and clipped actions in LDS with coalesced loads, each thread assembles its row of N*F + N - 1 values
 // in an LDS slab (odd row stride: no bank conflicts), and the block writes the slab, which is one
 // contiguous run of the output, with 16-byte stores. Used when the slab fits 48 KiB.
-template <typename OT, typename AT, int BS>
+template <typename OT, typename AT, int BS, bool NT = false>
 __global__ void __launch_bounds__(BS) imenv_cc_obs_slab_kernel(const OT* __restrict__ obs, const AT* __restrict__ act,
                                                                int64_t n, int N, int F, double lo, double hi,
                                                                OT* __restrict__ out) {
@@ -272,29 +272,32 @@ __global__ void __launch_bounds__(BS) imenv_cc_obs_slab_kernel(const OT* __restr
           v[u] = WP == W ? s_out[i] : s_out[(i / W) * WP + i % W];
         }
       }
-      if constexpr (V == 4) reinterpret_cast<float4*>(g)[q] = make_float4(v[0], v[1], v[2], v[3]);
-      else reinterpret_cast<double2*>(g)[q] = make_double2(v[0], v[1]);
+      if constexpr (V == 4) imenv::store16<NT>(reinterpret_cast<float4*>(g) + q, make_float4(v[0], v[1], v[2], v[3]));
+      else imenv::store16<NT>(reinterpret_cast<double2*>(g) + q, make_double2(v[0], v[1]));
     }
   } else {
     for (int i = tid; i < total; i += BS) g[i] = WP == W ? s_out[i] : s_out[(i / W) * WP + i % W];
   }
 }
 
-template <int BS>
+template <int BS, bool NT>
 void launch_cc_slab(dim3 g, size_t lds, hipStream_t st, const void* obs, int obs_dtype, const void* actions,
                     int action_dtype, int64_t n, int N, int F, double lo, double hi, void* out) {
   const dim3 b(BS);
   if (obs_dtype == IMENV_F32 && action_dtype == IMENV_F32)
-    hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<float, float, BS>), g, b, lds, st, static_cast<const float*>(obs),
-                       static_cast<const float*>(actions), n, N, F, lo, hi, static_cast<float*>(out));
+    hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<float, float, BS, NT>), g, b, lds, st,
+                       static_cast<const float*>(obs), static_cast<const float*>(actions), n, N, F, lo, hi,
+                       static_cast<float*>(out));
   else if (obs_dtype == IMENV_F32)
-    hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<float, double, BS>), g, b, lds, st, static_cast<const float*>(obs),
-                       static_cast<const double*>(actions), n, N, F, lo, hi, static_cast<float*>(out));
+    hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<float, double, BS, NT>), g, b, lds, st,
+                       static_cast<const float*>(obs), static_cast<const double*>(actions), n, N, F, lo, hi,
+                       static_cast<float*>(out));
   else if (action_dtype == IMENV_F32)
-    hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<double, float, BS>), g, b, lds, st, static_cast<const double*>(obs),
-                       static_cast<const float*>(actions), n, N, F, lo, hi, static_cast<double*>(out));
+    hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<double, float, BS, NT>), g, b, lds, st,
+                       static_cast<const double*>(obs), static_cast<const float*>(actions), n, N, F, lo, hi,
+                       static_cast<double*>(out));
   else
-    hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<double, double, BS>), g, b, lds, st,
+    hipLaunchKernelGGL((imenv_cc_obs_slab_kernel<double, double, BS, NT>), g, b, lds, st,
                        static_cast<const double*>(obs), static_cast<const double*>(actions), n, N, F, lo, hi,
                        static_cast<double*>(out));
 }
@@ -625,6 +628,7 @@ struct ImEnv {
   size_t demand_cap = 0;
   // kernel selection (imenv_set_jit): hipRTC-specialised kernels per JitFlags, else ahead-of-time
   int jit = 1;
+  int store_policy = IMENV_STORE_DEFAULT;   // imenv_set_store_policy
   bool jit_strict = false;   // IMENV_JIT_STRICT=1: a JIT failure is an error instead of an AOT fallback
   std::string arch;
   std::unordered_map<uint32_t, imenv::JitKernel> jit_k;
@@ -833,6 +837,7 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
     f.has_delay_u = A.delay_u != nullptr;
     f.demand_layout = A.demand_layout;
     f.metrics = A.metrics != nullptr;
+    f.stream_store = h->store_policy == IMENV_STORE_STREAM;
     auto it = h->jit_k.find(f.key());
     if (it == h->jit_k.end()) {
       // compiling + loading a module is not stream work: never do it while the stream is being
@@ -1011,10 +1016,16 @@ int imenv_cc_observation(int64_t n, int32_t num_agents, int32_t num_features, co
     const size_t lds = (size_t)E * N * 8 + (size_t)E * N * F * osz + (size_t)E * N * (W | 1) * osz;
     if (N <= 256 && lds <= 48 * 1024) {
       const dim3 g((unsigned)((n + E - 1) / E)), b(BSC);
+      // non-temporal row stores (default; IMENV_CC_NT=0 turns them off): the rows are read back only by
+      // a later training pass, and streamed past the caches the kernel runs at 76% of HBM peak instead
+      // of 54% (tools/bench_kernels.py, 2^20 envs, profiles/r02/kernels_cc_nt.log)
+      const bool nt = !(std::getenv("IMENV_CC_NT") && std::atoi(std::getenv("IMENV_CC_NT")) == 0);
       if (BSC == 512)
-        launch_cc_slab<512>(g, lds, st, obs, obs_dtype, actions, action_dtype, n, N, F, clip_lo, clip_hi, out);
+        launch_cc_slab<512, false>(g, lds, st, obs, obs_dtype, actions, action_dtype, n, N, F, clip_lo, clip_hi, out);
+      else if (nt)
+        launch_cc_slab<256, true>(g, lds, st, obs, obs_dtype, actions, action_dtype, n, N, F, clip_lo, clip_hi, out);
       else
-        launch_cc_slab<256>(g, lds, st, obs, obs_dtype, actions, action_dtype, n, N, F, clip_lo, clip_hi, out);
+        launch_cc_slab<256, false>(g, lds, st, obs, obs_dtype, actions, action_dtype, n, N, F, clip_lo, clip_hi, out);
       HIPCHK(hipGetLastError());
       return IMENV_OK;
     }
@@ -1178,6 +1189,14 @@ int imenv_set_delay_uniforms(ImEnv* h, int32_t period, const double* u, void* st
   return IMENV_OK;
 }
 
+int imenv_set_store_policy(ImEnv* h, int policy) {
+  if (!h) return fail(IMENV_E_INVALID, "null handle");
+  if (policy != IMENV_STORE_DEFAULT && policy != IMENV_STORE_STREAM)
+    return fail(IMENV_E_INVALID, "policy must be IMENV_STORE_DEFAULT or IMENV_STORE_STREAM");
+  h->store_policy = policy;
+  return IMENV_OK;
+}
+
 int imenv_set_jit(ImEnv* h, int mode) {
   if (!h) return fail(IMENV_E_INVALID, "null handle");
   if (mode != 0 && mode != 1) return fail(IMENV_E_INVALID, "mode must be 0 (ahead-of-time) or 1 (hipRTC)");
@@ -1217,6 +1236,7 @@ int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, cha
   f.noisy_demand = flags & 8u;
   f.has_delay_u = flags & 16u;
   f.metrics = flags & 1024u;
+  f.stream_store = flags & 2048u;
   f.demand_layout = (int)((flags >> 5) & 31u);
   std::string msg;
   std::string src;

@@ -50,12 +50,28 @@ typedef unsigned long long uint64_t;
 #include "imenv.h"
 
 #define IMENV_TABLE_MAX 1024
+#ifndef IMENV_NT_STORE
+#define IMENV_NT_STORE 0     // 1: observation / reward stores of the step kernel are non-temporal
+#endif
 #ifndef IMENV_WAVE_SLAB
 #define IMENV_WAVE_SLAB 0    // 1: each wave writes out its own staged observation rows (step_body)
 #endif
 #define IMENV_GUIDE_BITS 10
 
 namespace imenv {
+
+// 16-byte store, non-temporal under NT (streamed past the caches)
+template <bool NT, typename V>
+__device__ __forceinline__ void store16(V* p, const V& v) {
+  if constexpr (NT) {
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    u4 w;
+    __builtin_memcpy(&w, &v, 16);
+    __builtin_nontemporal_store(w, reinterpret_cast<u4*>(p));
+  } else {
+    *p = v;
+  }
+}
 
 struct SpecDev {
   ImEnvSpec s;
@@ -1015,6 +1031,8 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
     if (p.reward_mode() == IMENV_REWARD_INDEPENDENT) {
 #pragma unroll
       for (int i = 0; i < NT; ++i) if (i < N) A.reward[e * N + i] = prof[i];
+    } else if constexpr (IMENV_NT_STORE) {
+      __builtin_nontemporal_store(rew, A.reward + e);
     } else {
       A.reward[e] = rew;
     }
@@ -1239,7 +1257,8 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           // 16-byte stores need a 16-byte aligned destination (a caller's obs_out view may be offset)
           if ((total & 1) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0) {
             double2* g2 = reinterpret_cast<double2*>(gobs);
-            for (int q = gl; q < total / 2; q += GS) g2[q] = make_double2(at(so, 2 * q), at(so, 2 * q + 1));
+            for (int q = gl; q < total / 2; q += GS)
+              store16<IMENV_NT_STORE>(g2 + q, make_double2(at(so, 2 * q), at(so, 2 * q + 1)));
           } else {
             for (int q = gl; q < total; q += GS) gobs[q] = at(so, q);
           }
@@ -1263,10 +1282,11 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
             float4* g4 = reinterpret_cast<float4*>(gobs);
             if constexpr (SSTR == row) {
               const float4* s4 = reinterpret_cast<const float4*>(so);
-              for (int q = gl; q < total / 4; q += GS) g4[q] = s4[q];
+              for (int q = gl; q < total / 4; q += GS) store16<IMENV_NT_STORE>(g4 + q, s4[q]);
             } else {
               for (int q = gl; q < total / 4; q += GS)
-                g4[q] = make_float4(at(so, 4 * q), at(so, 4 * q + 1), at(so, 4 * q + 2), at(so, 4 * q + 3));
+                store16<IMENV_NT_STORE>(g4 + q, make_float4(at(so, 4 * q), at(so, 4 * q + 1), at(so, 4 * q + 2),
+                                                            at(so, 4 * q + 3)));
             }
           } else {
             for (int q = gl; q < total; q += GS) gobs[q] = at(so, q);

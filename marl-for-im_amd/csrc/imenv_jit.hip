@@ -201,6 +201,7 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
   // general observation rows staged in LDS and written as contiguous float4 / double2 runs (jit_obs_row)
   const int obs_row = jit_obs_row(d, base, bs, f.obs_f64 ? 8 : 4);
   const bool inline_tab = d.table_len <= kInlineTable;
+  if (f.stream_store) o << "#define IMENV_NT_STORE 1\n";
   o << "#include \"imenv_device.h\"\n"
        "// generated by imenv_jit.hip: every spec value is a compile-time constant\n"
        "struct JitSpec {\n";

@@ -310,6 +310,13 @@ class VectorInvEnv:
             per.append(b)
         return per
 
+    def set_store_policy(self, policy):
+        """"default": plain observation / reward stores (a policy reads them right after the step);
+        "stream": non-temporal stores for outputs bound for a rollout buffer read later (faster
+        step, slower immediate consumer). Same results either way."""
+        code = {"default": nat.STORE_DEFAULT, "stream": nat.STORE_STREAM}[policy]
+        nat.check(self.lib.imenv_set_store_policy(self._h, code), "imenv_set_store_policy")
+
     def set_jit(self, mode):
         """1: hipRTC kernel specialised for this spec (default); 0: ahead-of-time kernels."""
         nat.check(self.lib.imenv_set_jit(self._h, int(mode)), "imenv_set_jit")

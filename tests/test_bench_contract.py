@@ -49,6 +49,9 @@ def test_bench_json_line(steps, warmup):
     assert 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert r["kernel"].startswith("jit:imenv_step_jit")
     assert r["kernel_samples"] == steps and r["kernel_us"] > 0
+    assert r["store_policy"] == "default"
+    alt = r["alt_store_policy"]      # the other store policy, timed the same way (informational)
+    assert alt["store_policy"] == "stream" and alt["value"] > 0 and 0 < alt["frac"] < 1
     assert 90 < r["bytes_per_env_step"] <= r["bytes_per_env_step_steady"]
     if steps != 20:
         return

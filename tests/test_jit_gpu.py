@@ -115,3 +115,25 @@ def test_gpu_misaligned_obs_out_view(name, odt, mode):
     np.testing.assert_array_equal(view.cpu().numpy(), exp)
     for e in envs:
         e.close()
+
+
+@pytest.mark.parametrize("name", ["C2_MAIM4", "C3_IM8", "C4_MAIM_div1", "MAIM_div2_share", "MAIM4_indep"])
+@pytest.mark.parametrize("odt", ["f32", "f64"])
+def test_gpu_stream_store_policy_same_results(name, odt):
+    """IMENV_STORE_STREAM (non-temporal observation / reward stores) is a separate hipRTC kernel
+    (flag bit 0x800 in its tag) with bit-identical results; set back to the default, the plain
+    kernel runs again."""
+    from imenv import VectorInvEnv
+    meta, d = load_case(name)
+    tdt = torch.float64 if odt == "f64" else torch.float32
+    env = VectorInvEnv(meta["kind"], meta["config"], n_envs=meta["E"], device=DEV, obs_dtype=tdt)
+    env.set_store_policy("stream")
+    _episode(env, meta, d, tdt)
+    flags = int(re.search(r"flags=0x([0-9a-f]+)", env.kernel_info()).group(1), 16)
+    assert env.kernel_info().startswith("jit:") and flags & 0x800, env.kernel_info()
+    env.set_store_policy("default")
+    _episode(env, meta, d, tdt)
+    flags = int(re.search(r"flags=0x([0-9a-f]+)", env.kernel_info()).group(1), 16)
+    assert not flags & 0x800
+    assert env.lib.imenv_set_store_policy(env._h, 7) != 0      # unknown policy: IMENV_E_INVALID
+    env.close()
