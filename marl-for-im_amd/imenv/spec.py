@@ -198,7 +198,7 @@ def _common_tail(kind, g, N):
     return td, pa, pd, L
 
 
-def _demand_params(g, R, T):
+def _demand_params(g, R, T, serial=False):
     dist = g("demand_dist", "custom")
     if dist not in ("custom", "poisson", "uniform"):
         raise SpecError("Unrecognised, Distribution Not Implemented")   # IM_env.py:206-207
@@ -209,8 +209,8 @@ def _demand_params(g, R, T):
     custom = None
     if dist == "custom":
         cd = g("customer_demand", None)
-        if cd is None:
-            cd = np.ones((R, T)) * 5                 # IM_env.py:189 / IM_div_env.py:226 default
+        if cd is None:                               # IM_env.py:189 ([T]) / IM_div_env.py:226 ([R, T])
+            cd = np.ones(T) * 5 if serial else np.ones((R, T)) * 5
         custom = np.asarray(cd)
     return dist, mu, lu, custom
 
@@ -286,7 +286,7 @@ def _serial(kind, cfg):
             tail = [(nat.G_TRANSIT, k) for k in range(D)] if td else []
             tail += [(nat.G_ZERO, 0)] * (F - 3 - len(tail))
             feats += tail
-    dist, mu, lu, custom = _demand_params(g, 1, T)
+    dist, mu, lu, custom = _demand_params(g, 1, T, serial=True)
     return HostSpec(
         kind=kind, num_nodes=N, num_periods=T,
         parent=np.array([i + 1 for i in range(N - 1)] + [-1]),

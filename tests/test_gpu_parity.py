@@ -372,3 +372,33 @@ def test_gpu_output_buffers_are_checked_before_launch():
         env.reset(obs_out=torch.empty((128, 4, 3), device=DEV))
     assert env.state()["period"] == 0        # nothing was launched by the rejected calls
     env.close()
+
+
+@pytest.mark.parametrize("kind,cfg", [("MAIM", dict(C2, demand_dist="custom")), ("IM", dict(C3, demand_dist="custom")),
+                                      ("MAIM_div", dict(C4, demand_dist="custom")),
+                                      ("IM", dict(C3, demand_dist="custom", customer_demand=np.arange(30) % 7)),
+                                      ("MAIM_div", dict(C4, demand_dist="custom",
+                                                        customer_demand=np.arange(60).reshape(2, 30) % 9))])
+def test_gpu_custom_demand_from_config(kind, cfg):
+    """demand_dist "custom" with reset() and no demand argument: the config's customer_demand, or the
+    reference's default of 5 per period ([T] serial, IM_env.py:189; [R, T] tree, IM_div_env.py:226),
+    for every env of a batch."""
+    n = 64
+    env = _env(kind, cfg, n)
+    ora = OracleEnv(kind, cfg, n_envs=n)
+    serial = kind in ("IM", "MAIM")
+    T = env.T
+    dem = cfg.get("customer_demand", np.ones(T) * 5 if serial else np.ones((2, T)) * 5)
+    dem = np.broadcast_to(np.asarray(dem)[None], (n,) + np.asarray(dem).shape)
+    o0 = env.reset()
+    r0 = ora.reset(customer_demand=dem)
+    np.testing.assert_array_equal(o0.cpu().numpy().astype(np.float64), r0.astype(np.float32))
+    rs = np.random.RandomState(3)
+    for t in range(T):
+        a = rs.uniform(-1, 1, size=(n, env.N))
+        obs, rew, _, info = env.step(torch.as_tensor(a, device=DEV), info=True)
+        ro, rr, _, rinfo = ora.step(a)
+        np.testing.assert_array_equal(info["demand"].cpu().numpy().astype(np.float64), rinfo["demand"])
+        np.testing.assert_array_equal(obs.cpu().numpy(), ro.astype(np.float32))
+        np.testing.assert_array_equal(rew.cpu().numpy(), rr)
+    env.close()

@@ -2,7 +2,8 @@
 """Step-kernel roofline over every golden configuration (tests/golden: all four env classes and the
 observation-flag combinations the reference's scripts use), not only the bench workload.
 
-    python tools/bench_sweep.py [--n-envs 1048576] [--out gpurun_out/sweep.jsonl]
+    python tools/bench_sweep.py [--n-envs 1048576] [--out gpurun_out/sweep.jsonl] [--obs-f64] [--store stream]
+                                [--fuzz]
 
 Per config: float32 actions, float32 observations (--obs-f64: float64), in-kernel Philox demand (and noisy delay where the case
 has it), 2 warmup + 2 timed episodes; the step kernel is timed with HIP events on its stream over
@@ -22,15 +23,16 @@ for p in (ROOT, os.path.join(ROOT, "marl-for-im_amd"), os.path.join(ROOT, "tests
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from golden_io import case_names, load_case  # noqa: E402
+from golden_io import case_names, fuzz_case_names, load_case  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0
 
 
-def run_case(name, n, dev, obs_dtype=torch.float32):
+def run_case(name, n, dev, obs_dtype=torch.float32, store="default"):
     from imenv import VectorInvEnv
     meta, _ = load_case(name)
     env = VectorInvEnv(meta["kind"], meta["config"], n_envs=n, device=dev)
+    env.set_store_policy(store)
     N, T = env.N, env.T
     noisy = float(meta["noisy"])
     g = torch.Generator(device=dev)
@@ -60,7 +62,7 @@ def run_case(name, n, dev, obs_dtype=torch.float32):
                reward=("independent" if env.spec.reward_mode == 2 else "scalar"), noisy_delay=noisy,
                n_envs=n, kernel_us=round(us, 3), env_steps_per_s=round(n / (us * 1e-6), 1),
                bytes_per_env_step=round(avg, 3), achieved_gbs=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4),
-               kernel=env.kernel_info())
+               store_policy=store, kernel=env.kernel_info())
     env.close()
     return out
 
@@ -71,13 +73,15 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--cases", default=None, help="comma-separated subset")
     ap.add_argument("--obs-f64", action="store_true", help="float64 observations (the reference's dtype)")
+    ap.add_argument("--store", default="default", choices=["default", "stream"], help="step-kernel store policy")
+    ap.add_argument("--fuzz", action="store_true", help="also the drawn configurations of tests/golden/fuzz")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    names = args.cases.split(",") if args.cases else case_names()
+    names = args.cases.split(",") if args.cases else case_names() + (fuzz_case_names() if args.fuzz else [])
     fo = open(args.out, "w") if args.out else None
     for name in names:
-        r = run_case(name, args.n_envs, dev, torch.float64 if args.obs_f64 else torch.float32)
+        r = run_case(name, args.n_envs, dev, torch.float64 if args.obs_f64 else torch.float32, args.store)
         line = json.dumps(r)
         print(line, flush=True)
         if fo:
