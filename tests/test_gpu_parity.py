@@ -113,7 +113,10 @@ C4 = dict(num_nodes=4, connections={0: [1], 1: [2, 3], 2: [], 3: []}, num_period
 
 @pytest.mark.parametrize("kind,cfg,n", [("MAIM", C2, 8192), ("IM", C3, 4096), ("MAIM_div", C4, 8192),
                                          ("MAIM_div", dict(C4, noisy_demand=True, noisy_demand_threshold=0.3,
-                                                           demand_dist="uniform", lower_upper=(1, 9)), 4096)])
+                                                           demand_dist="uniform", lower_upper=(1, 9)), 4096),
+                                         ("IM", dict(C3, demand_dist="uniform", lower_upper=(2, 13)), 4096),
+                                         ("MAIM", dict(C2, mu=12.5, independent=True), 4096),
+                                         ("IM_div", dict(C4, mu=37.0, time_dependency=False), 4096)])
 def test_gpu_philox_rollout_matches_oracle(kind, cfg, n):
     """In-kernel Philox demand + f32 actions over two episodes == oracle with the same counters."""
     env = _env(kind, cfg, n, env_offset=1000)
