@@ -281,7 +281,9 @@ int imenv_column_stats(const double* x, int64_t rows, int32_t cols, double* out,
  *               [obs[e][o][0:F] for o != m] [obs[e][m][0:F]]        (o ascending)
  * obs: device [n][N][F] (obs_dtype), actions: device [n][N] (action_dtype) or NULL (zeros, as
  * central_critic_observer leaves them), out: device [n][N][N*F + N - 1] (obs_dtype). Works on any
- * row batch (e.g. a [T*n] rollout buffer); no env handle needed. */
+ * row batch (e.g. a [T*n] rollout buffer); no env handle needed. The rows are written with
+ * non-temporal stores (a later training pass reads them); IMENV_CC_NT=0 in the environment selects
+ * plain stores. */
 int imenv_cc_observation(int64_t n, int32_t num_agents, int32_t num_features, const void* obs, int obs_dtype,
                          const void* actions, int action_dtype, double clip_lo, double clip_hi, void* out,
                          void* stream);
@@ -292,7 +294,8 @@ int imenv_cc_observation(int64_t n, int32_t num_agents, int32_t num_features, co
  * rewards / values: device [T][n] (float32 or float64), last_value: device [n] bootstrap value
  * (value_dtype) or NULL for completed episodes (last_r = 0). Outputs float32 [T][n]: advantages and,
  * if not NULL, value_targets = advantages + values. Arithmetic follows the reference's NumPy / SciPy
- * dtypes and operation order (float64, or float32 deltas with a float32 bootstrap; imenv_gae_kernel). */
+ * dtypes and operation order (float64, or float32 deltas with a float32 bootstrap; imenv_gae_kernel).
+ * Outputs are written with non-temporal stores; IMENV_GAE_NT=0 selects plain stores. */
 int imenv_gae(int64_t n, int32_t T, const void* rewards, int reward_dtype, const void* values, int value_dtype,
               const void* last_value, double gamma, double lambda, float* advantages, float* value_targets,
               void* stream);
