@@ -7,6 +7,6 @@ mkdir -p $OUT
 for c in C3 C4; do
   timeout -k 10 300 python bench.py --config $c --cpu-seconds 1.0 > $OUT/bench_$c.json 2> $OUT/bench_$c.err || exit $?
   timeout -k 10 300 python bench.py --config $c --n-envs 1048576 --no-cpu-baseline > $OUT/bench_${c}_1M.json 2> $OUT/bench_${c}_1M.err || exit $?
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof_$c -o p --output-format csv -- python bench.py --config $c --n-envs 1048576 --no-cpu-baseline --steps 120 > $OUT/bench_prof_$c.json 2> $OUT/bench_prof_$c.err || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof_$c -o p --output-format csv -- python bench.py --config $c --n-envs 1048576 --no-cpu-baseline --no-alt-store --steps 120 > $OUT/bench_prof_$c.json 2> $OUT/bench_prof_$c.err || exit $?
 done
 echo "bench_configs done"

@@ -7,7 +7,7 @@ mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 &&
 timeout -k 10 180 python __graft_entry__.py smoke > $OUT/smoke.log 2>&1 &&
 timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o p --output-format csv -- python bench.py --no-cpu-baseline > $OUT/bench_prof.json 2> $OUT/bench_prof.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o p --output-format csv -- python bench.py --no-cpu-baseline --no-alt-store > $OUT/bench_prof.json 2> $OUT/bench_prof.err
 rc=$?
 echo "gpu_check rc=$rc"
 exit $rc

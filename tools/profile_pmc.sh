@@ -6,7 +6,7 @@ OUT=${1:-gpurun_out/pmc}
 export TMPDIR=/tmp
 mkdir -p $OUT
 python tools/pmc_calib.py build
-BENCH="python bench.py --no-cpu-baseline --steps 60 --warmup 30"
+BENCH="python bench.py --no-cpu-baseline --no-alt-store --steps 60 --warmup 30"
 run() { tag=$1; shift; timeout -k 10 240 rocprofv3 --pmc "$@" -d $GRAFT_REPO_ROOT/$OUT/$tag -o p --output-format csv -- $CMD > $OUT/$tag.log 2>&1; }
 CMD="python tools/pmc_calib.py"; run cal_fetch FETCH_SIZE; run cal_write WRITE_SIZE
 CMD=$BENCH; run fetch FETCH_SIZE; run write WRITE_SIZE
