@@ -303,12 +303,16 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
 }
 }  // namespace
 
+// the streaming-store variant has a name of its own, so kernel traces and PMC summaries never
+// average it with the plain-store kernel
+static const char* jit_kernel_name(const JitFlags& f) { return f.stream_store ? "imenv_step_jit_nt" : "imenv_step_jit"; }
+
 std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f) {
   std::ostringstream o;
   const int ept = jit_envs_per_thread(d, base, f.obs_f64);
   emit_policy(o, d, maxc, base, f, jit_step_block_size(d, base, f.obs_f64 ? 8 : 4, ept), ept);
   o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
-       "imenv_step_jit(const imenv::SpecDev* __restrict__ sp, const imenv::StepArgs A) {\n"
+    << jit_kernel_name(f) << "(const imenv::SpecDev* __restrict__ sp, const imenv::StepArgs A) {\n"
        "  __shared__ uint32_t s_tab[JitSpec::TAB_LDS];\n"
        "  __shared__ __attribute__((aligned(16))) float s_obs[imenv::stage_floats<JitSpec>()];\n"
        "  const JitSpec p(sp, A);\n"
@@ -418,13 +422,13 @@ bool load_module(const std::string& src, const std::string& arch, const char* fn
 bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const std::string& arch, JitKernel& out,
               std::string& msg) {
   const std::string src = jit_source(d, maxc, base, f);
-  if (!load_module(src, arch, "imenv_step_jit", out, msg)) return false;
+  if (!load_module(src, arch, jit_kernel_name(f), out, msg)) return false;
   out.ept = jit_envs_per_thread(d, base, f.obs_f64);
   out.bs = jit_step_block_size(d, base, f.obs_f64 ? 8 : 4, out.ept);
   char tag[160];
   // dev=: hash of the device-code header, so a profile of an older kernel body never matches this one
-  std::snprintf(tag, sizeof tag, "jit:imenv_step_jit[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,ept=%d,%zuB,dev=%08x]",
-                d.s.num_nodes, maxc, base ? 1 : 0, d.es, f.key(), out.bs, out.ept, src.size(), device_src_hash());
+  std::snprintf(tag, sizeof tag, "jit:%s[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,ept=%d,%zuB,dev=%08x]",
+                jit_kernel_name(f), d.s.num_nodes, maxc, base ? 1 : 0, d.es, f.key(), out.bs, out.ept, src.size(), device_src_hash());
   out.tag = tag;
   return true;
 }

@@ -53,7 +53,8 @@ def test_bench_json_line(steps, warmup):
     alt = r["alt_store_policy"]      # the other store policy, timed the same way (informational)
     assert alt["store_policy"] == "stream" and alt["value"] > 0 and 0 < alt["frac"] < 1
     # the line names the kernel it timed (plain stores), the informational run its own (flag 0x800)
-    assert ",flags=0x0," in r["kernel"] and ",flags=0x800," in alt["kernel"]
+    assert r["kernel"].startswith("jit:imenv_step_jit[") and ",flags=0x0," in r["kernel"]
+    assert alt["kernel"].startswith("jit:imenv_step_jit_nt[") and ",flags=0x800," in alt["kernel"]
     assert 90 < r["bytes_per_env_step"] <= r["bytes_per_env_step_steady"]
     if steps != 20:
         return
