@@ -1,7 +1,7 @@
 """GPU step kernels vs the oracle on randomly drawn specifications.
 
 The oracle is pinned to the reference on the committed fixtures, which include 26 drawn
-configurations (tests/golden/fuzz), and tools/fuzz_explore.py ran it against the reference on 500
+configurations (tests/golden/fuzz), and tools/fuzz_explore.py ran it against the reference on 1,400
 more drawn configurations without a mismatch. This test carries that coverage to the kernels:
 32 further drawn configurations (tests/fuzz_configs.py: all four classes, 2-8 stages or random
 trees, capacities 5-450, explicit order_max, delays 1-5, horizons 10-50, every observation flag,
