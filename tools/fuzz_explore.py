@@ -7,6 +7,7 @@ committed fixtures, so a configuration the oracle gets right the kernels are the
 
     python tools/fuzz_explore.py [num_configs] [seed]
 """
+import json
 import os
 import sys
 import traceback
@@ -42,7 +43,6 @@ def main():
         cfg = gz.maybe_order_max(rs, kind, cfg)
         opts = {"noisy": 0.3} if rs.rand() < 0.25 else {}
         gf.T = cfg["num_periods"]
-        import json
         try:
             ref = gf.run_case(classes, "x", kind, cfg, opts, seed=idx)
             meta = json.loads(str(ref.pop("meta")))
