@@ -157,6 +157,47 @@ class VectorInvEnv:
                   "imenv_set_delay_uniforms")
         self._keep_u = t
 
+    def rollout_stepper(self, actions, obs_out, reward_out):
+        """A launcher for step() over a rollout buffer whose tensors are validated once, here:
+        actions [T, n, N] float32 / float64, obs_out [T + 1, n, N, F] (row t + 1 receives the
+        observation after step t; row 0 is for reset(obs_out=obs_out[0])) or [T, n, N, F] (row t),
+        reward_out [T] + reward_shape(), all contiguous on this device. stepper(t) then launches the
+        step of period t with precomputed pointers on the current stream: one C call and no tensor
+        checks, for batches small enough that step()'s per-call host work (~9 us) would exceed the
+        kernel. t must be the handle's current period (0 after reset()). Returns done (period >= T)
+        like step(). Same kernels, same results as step()."""
+        T, n, N, F = self.T, self.n, self.N, self.F
+        ok = (torch.is_tensor(actions) and actions.device == self.device and actions.dtype in _FLOATS
+              and actions.is_contiguous() and tuple(actions.shape) == (T, n, N))
+        if not ok:
+            raise ValueError("actions must be a contiguous float32/float64 [%d, %d, %d] tensor on %s" % (T, n, N, self.device))
+        if not (torch.is_tensor(obs_out) and obs_out.device == self.device and obs_out.dtype in _FLOATS and
+                obs_out.is_contiguous() and tuple(obs_out.shape[1:]) == (n, N, F) and obs_out.shape[0] in (T, T + 1)):
+            raise ValueError("obs_out must be a contiguous float32/float64 [%d or %d, %d, %d, %d] tensor on %s"
+                             % (T + 1, T, n, N, F, self.device))
+        rshape = (T,) + self.reward_shape()
+        self._out(reward_out, rshape, (torch.float64,), "reward_out")
+        shift = 1 if obs_out.shape[0] == T + 1 else 0
+        a_ptr = [actions[t].data_ptr() for t in range(T)]
+        o_ptr = [obs_out[t + shift].data_ptr() for t in range(T)]
+        r_ptr = [reward_out[t].data_ptr() for t in range(T)]
+        adt = nat.F64 if actions.dtype == torch.float64 else nat.F32
+        odt = nat.F64 if obs_out.dtype == torch.float64 else nat.F32
+        lib, h, done, done_ref, stream = self.lib.imenv_step, self._h, self._done, self._done_ref, self._stream
+        keep = (actions, obs_out, reward_out)
+
+        def stepper(t):
+            if t != self.period:
+                raise ValueError("stepper(%d) at period %d: the kernel steps the handle's own period" % (t, self.period))
+            rc = lib(h, a_ptr[t], adt, o_ptr[t], odt, r_ptr[t], None, done_ref, stream())
+            if rc:
+                nat.check(rc, "imenv_step")
+            self.period += 1
+            return bool(done.value)
+
+        stepper.buffers = keep      # the tensors stay alive as long as the stepper
+        return stepper
+
     def step(self, actions, obs_out=None, reward_out=None, info=False, info_out=None):
         """step(action) (IM_env.py:287-360): actions [n, N] (or [n*N]) in the spec's action units.
 

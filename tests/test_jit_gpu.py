@@ -137,3 +137,40 @@ def test_gpu_stream_store_policy_same_results(name, odt):
     assert not flags & 0x800
     assert env.lib.imenv_set_store_policy(env._h, 7) != 0      # unknown policy: IMENV_E_INVALID
     env.close()
+
+
+@pytest.mark.parametrize("name", ["C2_MAIM4", "C4_MAIM_div1", "MAIM4_indep"])
+@pytest.mark.parametrize("odt", ["f32", "f64"])
+@pytest.mark.parametrize("rows", ["T+1", "T"])
+def test_gpu_rollout_stepper_matches_step(name, odt, rows):
+    """VectorInvEnv.rollout_stepper: the pre-validated launcher writes, period by period, exactly what
+    step() returns (the reference's golden observations and rewards), into rows t + 1 (or t) of the
+    bound buffers; a stepper called out of period order, and badly shaped buffers, are rejected."""
+    from imenv import VectorInvEnv
+    meta, d = load_case(name)
+    tdt = torch.float64 if odt == "f64" else torch.float32
+    E, T = meta["E"], meta["T"]
+    env = VectorInvEnv(meta["kind"], meta["config"], n_envs=E, device=DEV, obs_dtype=tdt)
+    acts = torch.as_tensor(d["actions"], dtype=torch.float64, device=DEV).permute(1, 0, 2).contiguous()
+    obs = torch.empty((T + 1 if rows == "T+1" else T, E, env.N, env.F), dtype=tdt, device=DEV)
+    rew = torch.empty((T,) + env.reward_shape(), dtype=torch.float64, device=DEV)
+    stepper = env.rollout_stepper(acts, obs, rew)
+    with pytest.raises(ValueError):
+        env.rollout_stepper(acts[:, :, :-1].contiguous(), obs, rew)
+    with pytest.raises(ValueError):
+        env.rollout_stepper(acts, obs[:, :, :, :-1].contiguous(), rew)
+    serial = meta["kind"] in ("IM", "MAIM")
+    dem = d["customer_demand"]
+    o0 = env.reset(customer_demand=dem[:, 0, :] if serial else dem)
+    with pytest.raises(ValueError):
+        stepper(1)
+    for t in range(T):
+        done = stepper(t)
+        assert done == (t == T - 1)
+    got = obs[1:] if rows == "T+1" else obs
+    exp = d["obs"] if tdt == torch.float64 else d["obs"].astype(np.float32)
+    np.testing.assert_array_equal(got.permute(1, 0, 2, 3).cpu().numpy(), exp)
+    r = rew.cpu().numpy()
+    r = r[..., None] if r.ndim == 2 else r
+    np.testing.assert_array_equal(np.transpose(r, (1, 0, 2)), d["reward"][..., :r.shape[-1]])
+    env.close()
