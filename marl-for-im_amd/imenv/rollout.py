@@ -40,12 +40,14 @@ class RolloutBuffer:
     """[T, n] episode storage on the env's device, shaped for VectorInvEnv.step's output arguments.
 
         buf = RolloutBuffer(env)                    # T = env.T periods, n = env.n envs
-        buf.obs[0] = env.reset()
+        env.reset(obs_out=buf.obs[0])
         for t in range(env.T):
             a, v = policy(buf.obs[t])
             buf.actions[t], buf.values[t] = a, v
-            env.step(a, obs_out=buf.obs[t + 1], reward_out=buf.rewards[t])
+            buf.step(t)                             # = env.step(buf.actions[t], obs_out=buf.obs[t + 1], ...)
         adv, vt = buf.advantages()
+
+    buf.step(t) launches period t through the env's rollout_stepper (buffers checked once, one C call).
     """
 
     def __init__(self, env, obs_dtype=torch.float32):
@@ -56,6 +58,11 @@ class RolloutBuffer:
         self.actions = torch.empty((T, n, N), dtype=torch.float32, device=dev)
         self.rewards = torch.empty((T,) + tuple(env.reward_shape()), dtype=torch.float64, device=dev)
         self.values = torch.empty((T, n), dtype=torch.float32, device=dev)
+        self._stepper = env.rollout_stepper(self.actions, self.obs, self.rewards)
+
+    def step(self, t):
+        """Step period t of the bound env from actions[t] into obs[t + 1] and rewards[t]; returns done."""
+        return self._stepper(t)
 
     def advantages(self, gamma=0.99, lambda_=0.95, last_value=None):
         r = self.rewards if self.rewards.dim() == 2 else self.rewards.sum(-1)

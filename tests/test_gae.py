@@ -81,4 +81,13 @@ def test_rollout_buffer_with_env():
     ea, ev = gae_batch(buf.rewards.cpu().numpy(), buf.values.cpu().numpy())
     np.testing.assert_array_equal(adv.cpu().numpy(), ea)
     np.testing.assert_array_equal(vt.cpu().numpy(), ev)
+    # the buffer's own launcher (RolloutBuffer.step -> rollout_stepper) fills a second buffer identically
+    env2 = VectorInvEnv("MAIM", gen_cfg.serial4(independent=False), n_envs=4096, device="cuda:0")
+    buf2 = RolloutBuffer(env2)
+    env2.reset(obs_out=buf2.obs[0])
+    buf2.actions.copy_(buf.actions)
+    for t in range(env2.T):
+        assert buf2.step(t) == (t == env2.T - 1)
+    assert torch.equal(buf2.obs, buf.obs) and torch.equal(buf2.rewards, buf.rewards)
     env.close()
+    env2.close()
