@@ -166,3 +166,40 @@ def test_rollout_errors():
     with pytest.raises(ValueError):
         ro.run(np.ones((1, 3)), n_scenarios=4)
     ro.close()
+
+
+@pytest.mark.parametrize("i", range(8))
+def test_rollout_drawn_configs_vs_oracle(i):
+    """The fused rollout on drawn single-agent configurations (tests/fuzz_configs.py: IM and IM_div,
+    capacities 5-450, explicit order_max, raw or standardised actions), in-kernel Poisson or uniform
+    demand, noisy demand on trees, noisy delay: every per-episode metric equals the oracle."""
+    from fuzz_configs import maybe_order_max, rand_config
+    rs = np.random.RandomState(4242 + i)
+    kind = ("IM", "IM_div")[i % 2]
+    while True:
+        cfg = maybe_order_max(rs, kind, rand_config(rs, kind, (i // 2) % 4))
+        R = sum(1 for v in cfg["connections"].values() if not v) if kind == "IM_div" else 1
+        if R * cfg["num_periods"] <= 128:       # the objective's pairwise-sum block
+            break
+    top = float(np.max(cfg["inv_max"]))
+    if i % 3 == 2:
+        lo = int(rs.randint(0, max(2, int(top // 4))))
+        cfg.update(demand_dist="uniform", lower_upper=(lo, lo + 2 + int(rs.randint(0, max(2, int(top // 2))))))
+    else:
+        cfg.update(demand_dist="poisson", mu=float(np.round(rs.uniform(0.05, 0.5) * top, 1)))
+    if kind == "IM_div" and rs.rand() < 0.5:
+        cfg.update(noisy_demand=True, noisy_demand_threshold=0.25)
+    thr = 0.3 if rs.rand() < 0.5 else 0.0
+    N = cfg.get("num_stages", cfg.get("num_nodes"))
+    P, S, off, ep = 3, 300, int(rs.randint(0, 1 << 20)), int(rs.randint(0, 50))
+    pol = rs.uniform(0, 1.5 * top, size=(P, N))
+    ro = _rollout(kind, cfg)
+    out = ro.run(pol, n_scenarios=S, scenario_offset=off, episode=ep, noisy_delay=thr > 0,
+                 noisy_delay_threshold=thr)
+    rng = dict(seed=cfg["seed"], episode=ep, env_offset=off, dist=cfg["demand_dist"], mu=cfg.get("mu", 5),
+               lower_upper=cfg.get("lower_upper", (1, 5)))
+    ref = bs.rollout(kind, cfg, pol, n_scenarios=S, rng=rng, pmf=_pmf(cfg), noisy_delay=thr > 0,
+                     noisy_delay_threshold=thr)
+    for k in STATS:
+        np.testing.assert_array_equal(out[k].cpu().numpy(), ref[k], err_msg="%d %s" % (i, k))
+    ro.close()
