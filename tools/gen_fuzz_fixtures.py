@@ -57,7 +57,7 @@ def rand_adaptor_config(rs, kind, idx):
     if tree and (idx // 4) % 2 == 0:       # cases 2, 3, 10, 11: custom, Poisson, uniform, custom demand
         cfg["noisy_demand"] = True
         cfg["noisy_demand_threshold"] = float(np.round(rs.uniform(0.05, 0.4), 2))
-    if kind == "MAIM_div" and rs.rand() < 0.4:
+    if tree and idx >= 6:        # cases 6, 7, 10, 11; both div envs read noisy_delay from the config (IM_div_env.py:50-51)
         cfg["noisy_delay"] = True
         cfg["noisy_delay_threshold"] = float(np.round(rs.uniform(0.05, 0.4), 2))
     opts = {"noisy": float(np.round(rs.uniform(0.1, 0.5), 2))} if rs.rand() < 0.3 else {}
