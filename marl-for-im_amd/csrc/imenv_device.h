@@ -1398,15 +1398,26 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
   double* __restrict__ my_terms = TBUF > 0 ? A.terms + (int64_t)blockIdx.x * (TBUF * BS) + tid : nullptr;
   // one term into np.sum's pairwise accumulators: 8 interleaved partial sums over the first `full`
   // indices, the rest kept for the sequential tail (NumPy's non-recursive block, n < 128)
+  // Terms arrive in index order 0, 1, 2, ... (each pass adds its row's T periods in order; TBUF adds
+  // rows 1.. after row 0), so accumulator idx & 7 is always the one at the front: add there and rotate
+  // the eight by one (1 add + 7 moves). After `full` (a multiple of 8) terms they are back in place.
+  // A (q == idx & 7) select over the eight would cost 8 adds + 16 v_cndmask per term.
   auto add_term = [&](const int idx, const double term) {
     if (idx < full) {
-      const int j = idx & 7;
+      const double a0 = acc8[0] + term;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) acc8[q] = (q == j) ? acc8[q] + term : acc8[q];
+      for (int q = 0; q < 7; ++q) acc8[q] = acc8[q + 1];
+      acc8[7] = a0;
     } else {
-      const int j = idx - full;
-#pragma unroll
-      for (int q = 0; q < 7; ++q) tail[q] = (q == j) ? term : tail[q];
+      switch (idx - full) {
+        case 0: tail[0] = term; break;
+        case 1: tail[1] = term; break;
+        case 2: tail[2] = term; break;
+        case 3: tail[3] = term; break;
+        case 4: tail[4] = term; break;
+        case 5: tail[5] = term; break;
+        default: tail[6] = term; break;
+      }
     }
   };
 #pragma unroll 1
