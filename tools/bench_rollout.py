@@ -128,6 +128,8 @@ def main():
                                "frac": round(ach / VALU_PEAK, 4),
                                "valu_instr_per_env_step": round(pmc["valu_wave_instr_per_launch"] * 64 / steps, 1),
                                "source": "profiles/pmc_rollout_kernel.json"}
+            if pmc.get("issue_model"):   # per-class issue costs (tools/probe_valu.hip): [low, high]
+                res["roofline"]["issue_model_frac"] = pmc["issue_model"]["frac"]
     except (OSError, ValueError, KeyError):
         pass
     if cpu:
