@@ -215,6 +215,35 @@ typedef struct ImEnvRollout {
   double* policy_stats;       /* out [P][IMENV_NUM_STATS][2]: np.mean, np.std over the S episodes, or NULL */
 } ImEnvRollout;
 
+/* Open-loop plan replay (imenv_plan_rollout): the LP scripts' evaluation loop, e.g. SHLP_8.py:737-766
+ * (also SHLP*.py, DSHLP*.py, Oracle*.py, DecLP.py, Distributed*_LP.py): per demand scenario
+ *   s = env.reset(customer_demand=d); step(plan[t]) for t < T;
+ *   lp_reward += r; total_inventory += sum(s[:, 0]); total_backlog += sum(s[:, 1]);
+ *   customer_backlog += s[0, 1]; profit[j, t] = r
+ * for num_plans x num_scenarios episodes in one launch (state in registers, lead-time queue in LDS).
+ * The inventory / backlog sums are of the state (= the scripts' observation sums, since every LP
+ * script runs with standardise_state False). */
+#define IMENV_PLAN_SHARED 0        /* actions [P][T][N]: plan p is replayed on every scenario */
+#define IMENV_PLAN_PER_EPISODE 1   /* actions [T][P][S][N]: each (plan row, scenario) episode has its own
+                                    * actions (an LP solved per demand scenario) */
+typedef struct ImEnvPlanRollout {
+  const void* actions;        /* device, action_dtype, layout plan_layout; decoded as step() decodes */
+  int32_t action_dtype;       /* IMENV_F32 / IMENV_F64 */
+  int32_t plan_layout;        /* IMENV_PLAN_* */
+  int64_t num_plans;          /* P >= 1 */
+  int64_t num_scenarios;      /* S >= 1 */
+  const int32_t* demand;      /* customer demand int32 [T][R][S] or NULL (drawn, as ImEnvRollout.demand) */
+  int64_t scenario_offset;
+  int64_t episode;
+  int32_t noisy_delay;        /* reset(noisy_delay=True, noisy_delay_threshold) */
+  int32_t pad_;
+  double noisy_delay_threshold;
+  double* rewards;            /* out double [T][P][S]: the per-step reward (profit[j, t]), or NULL */
+  double* episode_stats;      /* out [IMENV_NUM_STATS][P][S] (OBJECTIVE reads 0; CUSTOMER_BACKLOG is node 0's
+                               * backlog, s[0, 1]), or NULL */
+  double* policy_stats;       /* out [P][IMENV_NUM_STATS][2]: np.mean, np.std over the S episodes, or NULL */
+} ImEnvPlanRollout;
+
 /* Replaces the constructors: InvManagement.__init__ (IM_env.py:7-162),
  * MultiAgentInvManagement.__init__ (MAIM_env.py:8-173), InvManagementDiv.__init__
  * (IM_div_env.py:9-199), MultiAgentInvManagementDiv.__init__ (MAIM_div_env.py:9-237).
@@ -252,6 +281,12 @@ int imenv_step(ImEnv* env, const void* actions, int action_dtype, void* obs, int
  * SHARED_MEAN). Independent of the handle's own env state (it may be mid-episode); uses its spec,
  * device and kernel cache. Always runs a hipRTC-specialised kernel (IMENV_E_UNSUPPORTED without it). */
 int imenv_base_stock_rollout(ImEnv* env, const ImEnvRollout* args, void* stream);
+
+/* Replaces the LP scripts' plan replay loop (SHLP_8.py:737-766 and the scripts listed at
+ * ImEnvPlanRollout) for P plans x S scenarios in one fused launch (+ the stats reduction when
+ * policy_stats is given). Scalar-reward specs only. Like imenv_base_stock_rollout, independent of the
+ * handle's own env state; always hipRTC-specialised (IMENV_E_UNSUPPORTED without it). */
+int imenv_plan_rollout(ImEnv* env, const ImEnvPlanRollout* args, void* stream);
 
 /* Evaluation-harness metrics (inv_management.py:567-606, MA_inv_management.py:517-587,
  * MA_inv_management_div.py): with a buffer attached, every step() adds, per env, into row e of
@@ -358,8 +393,9 @@ int imenv_kernel_info(const ImEnv* env, char* buf, int64_t len);
  * `spec` for `arch` (e.g. "gfx950"); flags = bit0 f64 actions, bit1 f64 obs, bit2 noisy delay,
  * bit3 noisy demand, bit4 host-fed delay uniforms, bits 5-9 demand layout, bit10 episode metrics, bit11
  * streaming stores (IMENV_STORE_STREAM). With bit 12 set it
- * compiles the base-stock rollout kernel instead: bit13 demand table, bit14 noisy delay, bit15 noisy
- * demand, bit16 objective. `log` receives "ok" or
+ * compiles the rollout kernel instead: bit13 demand table, bit14 noisy delay, bit15 noisy
+ * demand, bit16 objective, bits 17-18 action source (0 base-stock, 1 shared plan, 2 per-episode
+ * plan), bit19 float64 plan actions. `log` receives "ok" or
  * the compiler log. */
 int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, char* log, int64_t log_len);
 

@@ -894,6 +894,9 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
   return IMENV_OK;
 }
 
+static int launch_rollout(ImEnv* h, const imenv::RolloutFlags& f, imenv::RolloutArgs A, double* policy_stats,
+                          hipStream_t st);
+
 int imenv_base_stock_rollout(ImEnv* h, const ImEnvRollout* r, void* stream) {
   if (!h || !r || !r->policy) return fail(IMENV_E_INVALID, "null argument");
   const ImEnvSpec& s = h->host.s;
@@ -916,6 +919,72 @@ int imenv_base_stock_rollout(ImEnv* h, const ImEnvRollout* r, void* stream) {
   f.noisy_delay = r->noisy_delay != 0;
   f.noisy_demand = !f.table && s.noisy_demand != 0;
   f.objective = r->demand_pmf != nullptr;
+  imenv::RolloutArgs A;
+  std::memset(&A, 0, sizeof(A));
+  A.policy = r->policy;
+  A.demand = r->demand;
+  A.pmf = r->demand_pmf;
+  A.pmf_len = r->demand_pmf ? r->pmf_len : 0;
+  A.ep = r->episode_stats;
+  A.S = r->num_scenarios;
+  A.P = r->num_policies;
+  A.scen_offset = (uint32_t)r->scenario_offset;
+  A.episode = (uint32_t)r->episode;
+  A.noisy_delay_thr32 = prob_thr32(r->noisy_delay_threshold);
+  return launch_rollout(h, f, A, r->policy_stats, st);
+}
+
+int imenv_plan_rollout(ImEnv* h, const ImEnvPlanRollout* r, void* stream) {
+  if (!h || !r || !r->actions) return fail(IMENV_E_INVALID, "null argument");
+  const ImEnvSpec& s = h->host.s;
+  if (s.reward_mode == IMENV_REWARD_INDEPENDENT)
+    return fail(IMENV_E_UNSUPPORTED, "plan rollout needs a scalar reward (independent multi-agent rewards)");
+  if (r->num_plans < 1 || r->num_scenarios < 1) return fail(IMENV_E_INVALID, "num_plans / num_scenarios < 1");
+  if (r->action_dtype != IMENV_F32 && r->action_dtype != IMENV_F64)
+    return fail(IMENV_E_INVALID, "action_dtype must be IMENV_F32 or IMENV_F64");
+  if (r->plan_layout != IMENV_PLAN_SHARED && r->plan_layout != IMENV_PLAN_PER_EPISODE)
+    return fail(IMENV_E_INVALID, "plan_layout must be IMENV_PLAN_SHARED or IMENV_PLAN_PER_EPISODE");
+  if (r->scenario_offset < 0 || r->scenario_offset + r->num_scenarios > (int64_t(1) << 32))
+    return fail(IMENV_E_INVALID, "scenario ids must fit 32 bits");
+  if (r->episode < 0 || r->episode > 0xFFFFFFFFll) return fail(IMENV_E_INVALID, "episode must fit 32 bits");
+  if (!r->demand && s.demand_dist != IMENV_DEMAND_POISSON && s.demand_dist != IMENV_DEMAND_UNIFORM)
+    return fail(IMENV_E_INVALID, "custom demand needs a table");
+  if (h->arch.empty()) return fail(IMENV_E_UNSUPPORTED, "plan rollout needs hipRTC (device arch unknown)");
+  {
+    // per-episode rows are loaded as whole 16 / 8-byte words (load_words), shared rows element-wise
+    const size_t row = (r->action_dtype == IMENV_F64 ? 8 : 4) * (size_t)s.num_nodes;
+    const size_t align = r->plan_layout == IMENV_PLAN_SHARED ? (r->action_dtype == IMENV_F64 ? 8 : 4)
+                         : row % 16 == 0 ? 16 : row % 8 == 0 ? 8 : 4;
+    if (reinterpret_cast<uintptr_t>(r->actions) % align)
+      return fail(IMENV_E_INVALID, "plan actions must be aligned to " + std::to_string(align) + " bytes");
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  HIPCHK(hipSetDevice(h->device));
+  imenv::RolloutFlags f;
+  f.table = r->demand != nullptr;
+  f.noisy_delay = r->noisy_delay != 0;
+  f.noisy_demand = !f.table && s.noisy_demand != 0;
+  f.act = r->plan_layout == IMENV_PLAN_SHARED ? imenv::ROLL_PLAN_SHARED : imenv::ROLL_PLAN_EPISODE;
+  f.act_f64 = r->action_dtype == IMENV_F64;
+  imenv::RolloutArgs A;
+  std::memset(&A, 0, sizeof(A));
+  A.plan = r->actions;
+  A.rewards = r->rewards;
+  A.demand = r->demand;
+  A.ep = r->episode_stats;
+  A.S = r->num_scenarios;
+  A.P = r->num_plans;
+  A.scen_offset = (uint32_t)r->scenario_offset;
+  A.episode = (uint32_t)r->episode;
+  A.noisy_delay_thr32 = prob_thr32(r->noisy_delay_threshold);
+  return launch_rollout(h, f, A, r->policy_stats, st);
+}
+
+// The fused rollout launch shared by the base-stock and plan rollouts: kernel lookup (compiled once per
+// flag set), per-block partials and parked-term scratch, the rollout kernel, then the stats merge.
+static int launch_rollout(ImEnv* h, const imenv::RolloutFlags& f, imenv::RolloutArgs A, double* policy_stats,
+                          hipStream_t st) {
+  const ImEnvSpec& s = h->host.s;
   auto it = h->roll_k.find(f.key());
   if (it == h->roll_k.end()) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -929,10 +998,9 @@ int imenv_base_stock_rollout(ImEnv* h, const ImEnvRollout* r, void* stream) {
     it = h->roll_k.emplace(f.key(), k).first;
   }
   const imenv::JitKernel& k = it->second;
-  const int64_t P = r->num_policies, S = r->num_scenarios;
+  const int64_t P = A.P, S = A.S;
   const int64_t bpp = (S + k.bs - 1) / k.bs;
   if (P * bpp > 0x7FFFFFFFll) return fail(IMENV_E_INVALID, "num_policies * ceil(num_scenarios / block) too large");
-  double* ep = r->episode_stats;
   const size_t pneed = (size_t)IMENV_NUM_STATS * P * bpp * 3;
   if (h->roll_part_cap < pneed) {
     if (h->d_roll_part) { HIPCHK(hipStreamSynchronize(st)); HIPCHK(hipFree(h->d_roll_part)); h->d_roll_part = nullptr; }
@@ -947,29 +1015,17 @@ int imenv_base_stock_rollout(ImEnv* h, const ImEnvRollout* r, void* stream) {
     if (rc) return rc;
     h->roll_terms_cap = tneed;
   }
-  imenv::RolloutArgs A;
-  std::memset(&A, 0, sizeof(A));
   A.terms = h->d_roll_terms;
-  A.policy = r->policy;
-  A.demand = r->demand;
-  A.pmf = r->demand_pmf;
-  A.pmf_len = r->demand_pmf ? r->pmf_len : 0;
-  A.ep = ep;
   A.partial = h->d_roll_part;
-  A.S = S;
-  A.P = P;
   A.bpp = bpp;
-  A.scen_offset = (uint32_t)r->scenario_offset;
-  A.episode = (uint32_t)r->episode;
   A.noisy_delay = f.noisy_delay ? 1 : 0;
   A.noisy_demand = f.noisy_demand ? 1 : 0;
-  A.noisy_delay_thr32 = prob_thr32(r->noisy_delay_threshold);
   A.noisy_demand_thr32 = prob_thr32(s.noisy_demand_threshold);
   HIPCHK(imenv::jit_rollout_launch(k, st, h->d_spec, A));
   h->last_rollout = k.tag;
-  if (r->policy_stats) {
+  if (policy_stats) {
     hipLaunchKernelGGL(imenv_rollout_stats_kernel, dim3((unsigned)P, IMENV_NUM_STATS), dim3(256), 0, st,
-                       h->d_roll_part, r->policy_stats, P, S, bpp);
+                       h->d_roll_part, policy_stats, P, S, bpp);
     HIPCHK(hipGetLastError());
   }
   return IMENV_OK;
@@ -1254,13 +1310,17 @@ int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, cha
   f.demand_layout = (int)((flags >> 5) & 31u);
   std::string msg;
   std::string src;
-  if (flags & (1u << 12)) {   // the base-stock rollout kernel; bits 13..17 = RolloutFlags::key()
+  if (flags & (1u << 12)) {   // the rollout kernel; bits 13..19 = RolloutFlags::key()
     imenv::RolloutFlags rf;
     const uint32_t rk = flags >> 13;
     rf.table = rk & 1u;
     rf.noisy_delay = rk & 2u;
     rf.noisy_demand = rk & 4u;
     rf.objective = rk & 8u;
+    rf.act = (int)((rk >> 4) & 3u);
+    rf.act_f64 = rk & 64u;
+    if (rf.act > imenv::ROLL_PLAN_EPISODE || (rf.act != imenv::ROLL_BASE_STOCK && rf.objective))
+      return fail(IMENV_E_INVALID, "rollout flags: unknown action source, or a plan with an objective");
     const int bs = imenv::rollout_block_size(d, rf);
     if (bs == 0) return fail(IMENV_E_UNSUPPORTED, "rollout does not fit LDS");
     src = imenv::jit_rollout_source(d, maxc, rf, bs);

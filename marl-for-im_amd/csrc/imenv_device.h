@@ -141,7 +141,9 @@ struct StepArgs {
 // Fused base-stock rollout (imenv_base_stock_rollout): whole episodes of P policies x S demand
 // scenarios in one launch, state in registers, the in-transit queue in LDS.
 struct RolloutArgs {
-  const double* policy;       // [P][N] order-up-to levels
+  const double* policy;       // [P][N] order-up-to levels (base-stock rollouts)
+  const void* plan;           // plan rollouts: [P][T][N] (PLAN_SHARED) or [T][P][S][N] (PLAN_PER_EPISODE) actions
+  double* rewards;            // [T][P][S] per-step rewards (plan rollouts), or null
   const int32_t* demand;      // [T][R][S] customer demand per scenario, or null: drawn in-kernel
   const double* pmf;          // [pmf_len] dfo_func weight of a customer-demand value (objective only)
   double* ep;                 // [IMENV_NUM_STATS][P][S] per-episode metrics, or null
@@ -1348,10 +1350,24 @@ __device__ __forceinline__ double block_sum(double v, double* s_red) {
 // and parks the terms of rows 1..R-1 in A.terms as [block][(r - 1) * T + t][thread] (TBUF = (R - 1) * T
 // doubles per thread: each block's scratch is one contiguous run, each wave store 512 contiguous
 // bytes), then adds them in index order after row 0's: the same np.sum order, one pass.
-template <class P, bool OBJ, int TBUF = 0>
+//
+// ACT selects where the actions come from:
+//   ROLL_BASE_STOCK    the order-up-to policy above (A.policy [P][N])
+//   ROLL_PLAN_SHARED   an open-loop plan per policy row, A.plan [P][T][N]: every scenario of block row
+//                      `pol` replays the same actions (wave-uniform address: one broadcast load)
+//   ROLL_PLAN_EPISODE  a plan per episode, A.plan [T][P][S][N]: the LP scripts' replay, where the plan
+//                      of demand scenario j is solved for that scenario (SHLP_8.py:737-766). Period
+//                      t+1's row is loaded while period t computes.
+// Plan actions go through decode_orders exactly as step() decodes its action argument. The plan
+// replays' customer backlog is node 0's backlog, as every LP script sums it (s[0, 1],
+// SHLP_8.py:754, SHLP_div1.py:587); base-stock rollouts keep the retailers' sum.
+constexpr int ROLL_BASE_STOCK = 0, ROLL_PLAN_SHARED = 1, ROLL_PLAN_EPISODE = 2;
+
+template <class P, bool OBJ, int TBUF = 0, int ACT = ROLL_BASE_STOCK>
 __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, const SpecDev* __restrict__ sp,
                                              uint32_t* s_thr, uint16_t* s_guide, int32_t* s_ring, double* s_pmf,
                                              int pmf_lds, double* s_red) {
+  static_assert(ACT == ROLL_BASE_STOCK || (!OBJ && TBUF == 0), "plan rollouts have no dfo objective");
   constexpr int NT = P::NT;
   constexpr int BS = P::BS;
   const int tid = threadIdx.x;
@@ -1382,7 +1398,34 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
 
   double lvl[NT];
 #pragma unroll
-  for (int i = 0; i < NT; ++i) lvl[i] = (i < N) ? A.policy[pol * N + i] : 0.0;
+  for (int i = 0; i < NT; ++i) lvl[i] = (ACT == ROLL_BASE_STOCK && i < N) ? A.policy[pol * N + i] : 0.0;
+  // Per-period inputs read from memory — the plan row (action words; float64: two per node) and the
+  // host demand table's entries — are loaded one period ahead: their HBM latency runs under a
+  // period of arithmetic. (Two periods ahead measured no faster: tools/bench_plan.py runs at
+  // 4.5-4.8 TB/s either way, the step kernel's level; it only costs registers.)
+  constexpr int AW = P::act_f64() ? 2 * NT : NT;
+  uint32_t pw[AW];
+  int dm[NT];
+  const int64_t PS = A.P * A.S;
+  const int64_t ep_row = pol * A.S + sl;            // this episode's row in a [T][P][S][N] plan
+  auto load_inputs = [&](const int t, uint32_t (&w)[AW], int (&dmt)[NT]) {
+    if constexpr (ACT == ROLL_PLAN_EPISODE) {
+      const int64_t off = ((int64_t)t * PS + ep_row) * NT;
+      if constexpr (P::act_f64()) load_words<8 * NT>(static_cast<const double*>(A.plan) + off, w);
+      else load_words<4 * NT>(static_cast<const float*>(A.plan) + off, w);
+    } else if constexpr (ACT == ROLL_PLAN_SHARED) {
+      const int64_t off = (pol * T + t) * NT;
+#pragma unroll
+      for (int q = 0; q < AW; ++q) w[q] = static_cast<const uint32_t*>(A.plan)[(P::act_f64() ? 2 : 1) * off + q];
+    }
+    if (!draw) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const int r = (i < N) ? p.retailer_slot(i) : -1;
+        dmt[i] = r >= 0 ? A.demand[((int64_t)t * R + r) * A.S + sl] : 0;
+      }
+    }
+  };
 
   const int n_terms = R * T;                       // np.sum over prob[R][T] * rewards[T]
   const int full = n_terms >= 8 ? n_terms - (n_terms % 8) : 0;
@@ -1432,6 +1475,7 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
     for (int i = 0; i < NT; ++i)
       if (i < N)
         for (int k = 0; k < p.delay(i); ++k) s_ring[(p.ring_off(i) + k) * BS + tid] = 0;
+    load_inputs(0, pw, dm);
 
     uint4 rb_dem[NT], rb_dbl[NT], rb_zero[NT];   // one Philox block per 4 periods
     uint4 rb_delay[(NT + 3) / 4];                 // noisy delay: one block per 4 nodes per period
@@ -1471,7 +1515,7 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
           if (r >= 0) {
             int cd;
             if (!draw) {
-              cd = A.demand[((int64_t)t * R + r) * A.S + sl];
+              cd = dm[i];
             } else {
               const uint32_t w = word_of(rb_dem[i], tw);
               if (poisson) {
@@ -1490,16 +1534,23 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
           const int d = p.delay(i);
           if (t >= d) arr[i] = s_ring[(p.ring_off(i) + t % d) * BS + tid];
           if (p.noisy_delay() && t >= d) defer[i] = (uint64_t)word_of(rb_delay[i >> 2], i & 3) < A.noisy_delay_thr32;
-          // base_stock_policy (base_restock_policy.py:12-20): order up to lvl from the echelon position
-          // inv + order_u - backlog (integers: exact, as the reference's float64 sum of integers),
-          // min(order_max, max(policy - position, 0)); then the env's decode
-          const double om = (double)p.order_max(i);
-          const double xa = fmin(om, fmax(lvl[i] - (double)(inv[i] + ou[i] - bl[i]), 0.0));
-          if (p.std_actions()) x[i] = xa;
-          else order[i] = (int)rint(xa);   // unstandardised: the decode's clip is a no-op on [0, om]
+          if constexpr (ACT == ROLL_BASE_STOCK) {
+            // base_stock_policy (base_restock_policy.py:12-20): order up to lvl from the echelon position
+            // inv + order_u - backlog (integers: exact, as the reference's float64 sum of integers),
+            // min(order_max, max(policy - position, 0)); then the env's decode
+            const double om = (double)p.order_max(i);
+            const double xa = fmin(om, fmax(lvl[i] - (double)(inv[i] + ou[i] - bl[i]), 0.0));
+            if (p.std_actions()) x[i] = xa;
+            else order[i] = (int)rint(xa);   // unstandardised: the decode's clip is a no-op on [0, om]
+          } else if constexpr (P::act_f64()) {
+            x[i] = __hiloint2double((int)pw[2 * i + 1], (int)pw[2 * i]);
+          } else {
+            x[i] = (double)__uint_as_float(pw[i]);   // float32 plans promote exactly, as step() does
+          }
         }
       }
-      if (p.std_actions()) decode_orders(p, x, order);
+      if (t + 1 < T) load_inputs(t + 1, pw, dm);   // period t + 1's loads under this period's work
+      if (ACT != ROLL_BASE_STOCK || p.std_actions()) decode_orders(p, x, order);
       int dem[NT], acq[NT], ship[NT], sto[NT], cout[NT], push[NT];
       double prof[NT];
       double rew;
@@ -1520,10 +1571,12 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
           if (i < N) {
             inv_s += inv[i];
             bl_s += bl[i];
-            if (p.retailer_slot(i) >= 0) cbl_s += bl[i];
+            if (ACT == ROLL_BASE_STOCK ? p.retailer_slot(i) >= 0 : i == 0) cbl_s += bl[i];
           }
         }
         ret += rew;
+        // the LP scripts' per-step record, profit[j, t] = r (SHLP_8.py:751): one coalesced row per period
+        if (ACT != ROLL_BASE_STOCK && A.rewards && valid) A.rewards[(int64_t)t * PS + ep_row] = rew;
       }
       if constexpr (OBJ) {
 #pragma unroll
@@ -1558,7 +1611,6 @@ __device__ __forceinline__ void rollout_body(const P& p, const RolloutArgs& A, c
 
   const double v[IMENV_NUM_STATS] = {ret, obj, (double)inv_s, (double)bl_s, (double)cbl_s};
   if (A.ep && valid) {
-    const int64_t PS = A.P * A.S;
 #pragma unroll
     for (int m = 0; m < IMENV_NUM_STATS; ++m) A.ep[m * PS + pol * A.S + s] = v[m];
   }

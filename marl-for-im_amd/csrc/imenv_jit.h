@@ -65,8 +65,11 @@ struct RolloutFlags {
   bool noisy_delay = false;
   bool noisy_demand = false;  // drawn demand only
   bool objective = false;     // dfo_func objective (pmf given)
+  int act = ROLL_BASE_STOCK;  // action source (rollout_body ACT): base-stock policy or an open-loop plan
+  bool act_f64 = false;       // plan actions are float64 (else float32)
   uint32_t key() const {
-    return (table ? 1u : 0u) | (noisy_delay ? 2u : 0u) | (noisy_demand ? 4u : 0u) | (objective ? 8u : 0u);
+    return (table ? 1u : 0u) | (noisy_delay ? 2u : 0u) | (noisy_demand ? 4u : 0u) | (objective ? 8u : 0u) |
+           ((uint32_t)act << 4) | (act_f64 ? 64u : 0u);
   }
 };
 

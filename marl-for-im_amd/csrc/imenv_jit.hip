@@ -467,6 +467,7 @@ std::string jit_rollout_source(const SpecDev& d, int maxc, const RolloutFlags& f
   jf.noisy_delay = f.noisy_delay;
   jf.noisy_demand = f.noisy_demand;
   jf.demand_layout = f.table ? IMENV_LAYOUT_PER_ENV : IMENV_LAYOUT_DRAW;
+  jf.act_f64 = f.act_f64;
   std::ostringstream o;
   emit_policy(o, d, maxc, false, jf, bs, 1);
   const int pmf = f.objective ? kRolloutPmfLds : 1;
@@ -486,7 +487,7 @@ std::string jit_rollout_source(const SpecDev& d, int maxc, const RolloutFlags& f
        "  __shared__ double s_red[JitSpec::BS / 64];\n"
        "  const JitSpec p(sp, A);\n"
        "  imenv::rollout_body<JitSpec, "
-    << blit(f.objective) << ", " << tb << ">(p, A, sp, s_thr, s_guide, s_ring, s_pmf, " << pmf
+    << blit(f.objective) << ", " << tb << ", " << f.act << ">(p, A, sp, s_thr, s_guide, s_ring, s_pmf, " << pmf
     << ", s_red);\n"
        "}\n";
   return o.str();

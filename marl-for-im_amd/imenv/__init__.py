@@ -11,6 +11,7 @@ imenv_capi.hip; declared in include/imenv.h) driven from Python. Public surface:
   BaseStockRollout, dfo_func, base_stock_policy,
   optimize_inventory_policy     base-stock policy search on the GPU (policy.py,
                                 base_restock_policy.py's interface)
+  PlanRollout, replay_plans     the LP scripts' plan replay loop on the GPU (plan.py)
 
 torch is imported lazily so that the spec builder works without a GPU stack.
 """
@@ -29,4 +30,7 @@ def __getattr__(name):
                 "evaluate_base_stock"):
         from . import policy
         return getattr(policy, name)
+    if name in ("PlanRollout", "replay_plans"):
+        from . import plan
+        return getattr(plan, name)
     raise AttributeError(name)

@@ -29,6 +29,7 @@ DEMAND_CUSTOM, DEMAND_POISSON, DEMAND_UNIFORM = 1, 2, 3
 LAYOUT_DRAW, LAYOUT_PER_ENV, LAYOUT_BROADCAST = 0, 1, 2
 F32, F64 = 0, 1
 STORE_DEFAULT, STORE_STREAM = 0, 1
+PLAN_SHARED, PLAN_PER_EPISODE = 0, 1
 STAT_RETURN, STAT_OBJECTIVE, STAT_INVENTORY, STAT_BACKLOG, STAT_CUSTOMER_BACKLOG = range(5)
 NUM_STATS = 5
 STAT_NAMES = ("return", "objective", "inventory", "backlog", "customer_backlog")
@@ -72,6 +73,14 @@ class ImEnvRollout(ctypes.Structure):
                 ("noisy_delay_threshold", c_double), ("episode_stats", c_void_p), ("policy_stats", c_void_p)]
 
 
+class ImEnvPlanRollout(ctypes.Structure):
+    _fields_ = [("actions", c_void_p), ("action_dtype", c_int32), ("plan_layout", c_int32),
+                ("num_plans", c_int64), ("num_scenarios", c_int64), ("demand", c_void_p),
+                ("scenario_offset", c_int64), ("episode", c_int64), ("noisy_delay", c_int32), ("pad_", c_int32),
+                ("noisy_delay_threshold", c_double), ("rewards", c_void_p), ("episode_stats", c_void_p),
+                ("policy_stats", c_void_p)]
+
+
 # (name, restype, argtypes) for every symbol include/imenv.h declares
 SYMBOLS = [
     ("imenv_create", c_int, [POINTER(ImEnvSpec), c_int64, c_int64, c_int, POINTER(c_void_p)]),
@@ -80,6 +89,7 @@ SYMBOLS = [
     ("imenv_step", c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, POINTER(ImEnvInfo),
                            POINTER(c_int32), c_void_p]),
     ("imenv_base_stock_rollout", c_int, [c_void_p, POINTER(ImEnvRollout), c_void_p]),
+    ("imenv_plan_rollout", c_int, [c_void_p, POINTER(ImEnvPlanRollout), c_void_p]),
     ("imenv_set_episode_metrics", c_int, [c_void_p, c_void_p]),
     ("imenv_column_stats", c_int, [c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
     ("imenv_cc_observation", c_int, [c_int64, c_int32, c_int32, c_void_p, c_int, c_void_p, c_int, c_double, c_double,

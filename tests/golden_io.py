@@ -20,7 +20,7 @@ def decode_config(cfg):
     return out
 
 
-NON_CASE = ("base_stock", "cc_obs")   # gen_base_stock_fixtures.py / gen_cc_fixtures.py (own loaders)
+NON_CASE = ("base_stock", "cc_obs", "plan_replay")   # gen_base_stock / gen_cc / gen_plan_fixtures.py (own loaders)
 
 
 def case_names():
@@ -57,9 +57,10 @@ def load_adaptor_case(name):
     return meta, d
 
 
-def load_base_stock():
-    """tests/golden/base_stock.npz (tools/gen_base_stock_fixtures.py): {case: {field: array}}, meta."""
-    z = np.load(os.path.join(GOLDEN, "base_stock.npz"), allow_pickle=False)
+def load_base_stock(fname="base_stock.npz"):
+    """tests/golden/base_stock.npz (tools/gen_base_stock_fixtures.py) or plan_replay.npz
+    (tools/gen_plan_fixtures.py): {case: {field: array}}, meta."""
+    z = np.load(os.path.join(GOLDEN, fname), allow_pickle=False)
     meta = json.loads(str(z["meta"]))
     cases = {}
     for k in z.files:

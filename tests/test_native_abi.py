@@ -91,3 +91,24 @@ def test_jit_rollout_kernel_compiles_for_scalar_reward_specs():
             flags = (1 << 12) | (rk << 13)
             rc = lib.imenv_jit_check(ctypes.byref(spec), b"gfx950", flags, log, len(log))
             assert rc == 0, (name, rk, log.value.decode()[:2000])
+
+
+def test_jit_plan_rollout_kernel_compiles():
+    """hipRTC builds the plan-replay form of the rollout kernel (ACT = shared / per-episode plan,
+    float32 and float64 plans) for the golden plan-replay specs and the bench's C2 spec."""
+    from golden_io import load_base_stock
+    from imenv import _native, build_spec
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libimenv.so not built")
+    lib = _native.load()
+    log = ctypes.create_string_buffer(1 << 16)
+    meta, _ = load_base_stock("plan_replay.npz")
+    for name, m in sorted(meta.items()):
+        spec = build_spec(m["kind"], m["config"]).to_c()
+        for rk in (1 | (1 << 4) | 64, 1 | (2 << 4), 2 | (2 << 4) | 64):
+            flags = (1 << 12) | (rk << 13)
+            rc = lib.imenv_jit_check(ctypes.byref(spec), b"gfx950", flags, log, len(log))
+            assert rc == 0, (name, rk, log.value.decode()[:2000])
+    # a plan rollout with an objective is not a kernel
+    spec = build_spec(meta["SHLP4"]["kind"], meta["SHLP4"]["config"]).to_c()
+    assert lib.imenv_jit_check(ctypes.byref(spec), b"gfx950", (1 << 12) | ((8 | (2 << 4)) << 13), log, len(log)) != 0
