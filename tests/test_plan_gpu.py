@@ -153,3 +153,24 @@ def test_plan_replay_errors():
     with pytest.raises(ValueError):
         pr.run(np.ones((30, 4)))                                     # shared plan, no scenario count
     pr.close()
+
+
+def test_plan_replay_sharded_scenarios_equal_one_launch():
+    """Scenarios split across two launches (scenario_offset = a rank's first global scenario id, as
+    imenv.shard assigns them) give the same per-episode values and rewards as one launch over all of
+    them: the in-kernel draws are keyed by global scenario id."""
+    import gen_cfg
+    cfg = gen_cfg.div1(standardise_state=False, standardise_actions=False, noisy_demand=True,
+                       noisy_demand_threshold=0.2)
+    S, T, N, half = 1000, 30, 4, 400
+    rs = np.random.RandomState(11)
+    plans = rs.randint(0, 20, size=(1, S, T, N)).astype(np.float64)
+    pr = _pr("IM_div", cfg)
+    whole = pr.run(plans, per_episode=True, n_scenarios=S, episode=5, noisy_delay=True, noisy_delay_threshold=0.2)
+    a = pr.run(plans[:, :half], per_episode=True, n_scenarios=half, episode=5, noisy_delay=True,
+               noisy_delay_threshold=0.2)
+    b = pr.run(plans[:, half:], per_episode=True, n_scenarios=S - half, scenario_offset=half, episode=5,
+               noisy_delay=True, noisy_delay_threshold=0.2)
+    for k in STATS + ("rewards",):
+        np.testing.assert_array_equal(torch.cat([a[k], b[k]], 1).cpu().numpy(), whole[k].cpu().numpy(), err_msg=k)
+    pr.close()
