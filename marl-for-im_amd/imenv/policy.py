@@ -87,13 +87,18 @@ class BaseStockRollout:
         return d[:, :, :T].to(device=self.device, dtype=torch.int32).permute(2, 1, 0).contiguous()
 
     def run(self, policies, demand=None, n_scenarios=None, scenario_offset=0, episode=0, noisy_delay=False,
-            noisy_delay_threshold=0.0, objective=True, per_episode=True, stream=None):
+            noisy_delay_threshold=0.0, objective=True, per_episode=True, stream=None, check_finite=True):
+        """check_finite: raise ValueError for non-finite policies. Host inputs are checked on the host;
+        a device tensor costs a device-to-host sync per call (a caller that validated its tensor once,
+        e.g. a timing loop, passes False)."""
+        if check_finite and not torch.is_tensor(policies) and not np.isfinite(np.asarray(policies, dtype=np.float64)).all():
+            raise ValueError("policies must be finite")
         p = torch.as_tensor(policies, dtype=torch.float64, device=self.device)
         if p.dim() == 1:
             p = p.unsqueeze(0)
         if p.dim() != 2 or p.shape[1] != self.N:
             raise ValueError("policies must be [P, %d]" % self.N)
-        if not torch.isfinite(p).all():
+        if check_finite and torch.is_tensor(policies) and not torch.isfinite(p).all():
             raise ValueError("policies must be finite")
         p = p.contiguous()
         P = p.shape[0]

@@ -174,3 +174,51 @@ def test_plan_replay_sharded_scenarios_equal_one_launch():
     for k in STATS + ("rewards",):
         np.testing.assert_array_equal(torch.cat([a[k], b[k]], 1).cpu().numpy(), whole[k].cpu().numpy(), err_msg=k)
     pr.close()
+
+
+@pytest.mark.parametrize("i", range(8))
+def test_plan_replay_drawn_configs_vs_oracle(i):
+    """Plan replays on drawn configurations of all four classes (tests/fuzz_configs.py: 2-8 stages,
+    random trees, capacities 5-450 (uint8 and int16 state), delays 1-5, horizons 10-50, raw or
+    standardised actions, shared rewards for the multi-agent classes, explicit order_max), in-kernel
+    Poisson / uniform demand, noisy demand on trees, noisy delay; plans drawn around the action range
+    (standardised: beyond [a, b]; raw: beyond [0, order_max], fractional). Every per-episode value and
+    per-step reward equals the oracle."""
+    from fuzz_configs import maybe_order_max, rand_config
+    rs = np.random.RandomState(9090 + i)
+    kind = ("IM", "IM_div", "MAIM", "MAIM_div")[i % 4]
+    cfg = maybe_order_max(rs, kind, rand_config(rs, kind, (i + i // 4) % 4))   # capacities 5-450
+    if kind in ("MAIM", "MAIM_div"):
+        cfg["independent"] = False           # the rollout needs a scalar reward
+    top = float(np.max(cfg["inv_max"]))
+    if i % 3 == 2:
+        lo = int(rs.randint(0, max(2, int(top // 4))))
+        cfg.update(demand_dist="uniform", lower_upper=(lo, lo + 2 + int(rs.randint(0, max(2, int(top // 2))))))
+    else:
+        cfg.update(demand_dist="poisson", mu=float(np.round(rs.uniform(0.05, 0.5) * top, 1)))
+    if kind in ("IM_div", "MAIM_div") and rs.rand() < 0.5:
+        cfg.update(noisy_demand=True, noisy_demand_threshold=0.25)
+    thr = 0.3 if rs.rand() < 0.5 else 0.0
+    N = cfg.get("num_stages", cfg.get("num_nodes"))
+    T = cfg["num_periods"]
+    P, S, off, ep = 2, 256 + 37, int(rs.randint(0, 1 << 20)), int(rs.randint(0, 50))
+    per_episode = bool(i % 2)
+    shape = (P, S, T, N) if per_episode else (P, T, N)
+    std = cfg.get("standardise_actions", True) or kind == "MAIM_div"
+    if std:
+        a, b = cfg.get("a", -1.0), cfg.get("b", 1.0)
+        plans = rs.uniform(a - 0.3 * (b - a), b + 0.3 * (b - a), size=shape)
+    else:
+        plans = rs.uniform(-0.2 * top, 1.2 * top, size=shape)
+    pr = _pr(kind, cfg)
+    out = pr.run(plans, n_scenarios=S, scenario_offset=off, episode=ep, per_episode=per_episode,
+                 noisy_delay=thr > 0, noisy_delay_threshold=thr)
+    rng = dict(seed=cfg["seed"], episode=ep, env_offset=off, dist=cfg["demand_dist"], mu=cfg.get("mu", 5),
+               lower_upper=cfg.get("lower_upper", (1, 5)))
+    ref_plans = np.transpose(plans, (2, 0, 1, 3)) if per_episode else plans
+    ref = pl.plan_rollout(kind, cfg, ref_plans, per_episode=per_episode, n_scenarios=S, rng=rng,
+                          noisy_delay=thr > 0, noisy_delay_threshold=thr)
+    for k in STATS:
+        np.testing.assert_array_equal(out[k].cpu().numpy(), ref[k], err_msg=k)
+    np.testing.assert_array_equal(out["rewards"].cpu().numpy(), np.transpose(ref["rewards"], (1, 2, 0)))
+    pr.close()

@@ -8,7 +8,7 @@ mkdir -p $OUT
 B="python tools/bench_rollout.py --no-cpu --reps 5"
 # instruction-class counters (8 SQ counters: the per-pass limit); tools/bin/probe_valu prices each class
 CLASSES="SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64"
-test -x tools/bin/probe_valu || hipcc --offload-arch=gfx950 -O3 -o tools/bin/probe_valu tools/probe_valu.hip
+mkdir -p tools/bin; test -x tools/bin/probe_valu || hipcc --offload-arch=gfx950 -O3 -o tools/bin/probe_valu tools/probe_valu.hip
 timeout -k 10 300 python tools/bench_rollout.py > $OUT/bench.json 2> $OUT/bench.err &&
 timeout -k 10 300 python tools/bench_rollout.py --config IM8 --no-cpu > $OUT/bench_im8.json 2>> $OUT/bench.err &&
 timeout -k 10 300 python tools/bench_rollout.py --config IM_div1 --no-cpu > $OUT/bench_div1.json 2>> $OUT/bench.err &&
