@@ -176,16 +176,12 @@ def test_plan_replay_sharded_scenarios_equal_one_launch():
     pr.close()
 
 
-@pytest.mark.parametrize("i", range(8))
-def test_plan_replay_drawn_configs_vs_oracle(i):
-    """Plan replays on drawn configurations of all four classes (tests/fuzz_configs.py: 2-8 stages,
-    random trees, capacities 5-450 (uint8 and int16 state), delays 1-5, horizons 10-50, raw or
-    standardised actions, shared rewards for the multi-agent classes, explicit order_max), in-kernel
-    Poisson / uniform demand, noisy demand on trees, noisy delay; plans drawn around the action range
-    (standardised: beyond [a, b]; raw: beyond [0, order_max], fractional). Every per-episode value and
-    per-step reward equals the oracle."""
+def drawn_plan_case(seed, i):
+    """One drawn plan-replay case (class i % 4, capacity scale by i): returns (kernel outputs as NumPy,
+    oracle outputs, kind). Shared by test_plan_replay_drawn_configs_vs_oracle and
+    tools/fuzz_plan_campaign.py."""
     from fuzz_configs import maybe_order_max, rand_config
-    rs = np.random.RandomState(9090 + i)
+    rs = np.random.RandomState(seed)
     kind = ("IM", "IM_div", "MAIM", "MAIM_div")[i % 4]
     cfg = maybe_order_max(rs, kind, rand_config(rs, kind, (i + i // 4) % 4))   # capacities 5-450
     if kind in ("MAIM", "MAIM_div"):
@@ -210,15 +206,30 @@ def test_plan_replay_drawn_configs_vs_oracle(i):
         plans = rs.uniform(a - 0.3 * (b - a), b + 0.3 * (b - a), size=shape)
     else:
         plans = rs.uniform(-0.2 * top, 1.2 * top, size=shape)
+    if rs.rand() < 0.5:
+        plans = plans.astype(np.float32)
     pr = _pr(kind, cfg)
     out = pr.run(plans, n_scenarios=S, scenario_offset=off, episode=ep, per_episode=per_episode,
                  noisy_delay=thr > 0, noisy_delay_threshold=thr)
+    got = {k: out[k].cpu().numpy() for k in STATS + ("rewards",)}
+    pr.close()
     rng = dict(seed=cfg["seed"], episode=ep, env_offset=off, dist=cfg["demand_dist"], mu=cfg.get("mu", 5),
                lower_upper=cfg.get("lower_upper", (1, 5)))
     ref_plans = np.transpose(plans, (2, 0, 1, 3)) if per_episode else plans
-    ref = pl.plan_rollout(kind, cfg, ref_plans, per_episode=per_episode, n_scenarios=S, rng=rng,
+    ref = pl.plan_rollout(kind, cfg, ref_plans.astype(np.float64), per_episode=per_episode, n_scenarios=S, rng=rng,
                           noisy_delay=thr > 0, noisy_delay_threshold=thr)
-    for k in STATS:
-        np.testing.assert_array_equal(out[k].cpu().numpy(), ref[k], err_msg=k)
-    np.testing.assert_array_equal(out["rewards"].cpu().numpy(), np.transpose(ref["rewards"], (1, 2, 0)))
-    pr.close()
+    ref["rewards"] = np.transpose(ref["rewards"], (1, 2, 0))
+    return got, ref, kind
+
+
+@pytest.mark.parametrize("i", range(8))
+def test_plan_replay_drawn_configs_vs_oracle(i):
+    """Plan replays on drawn configurations of all four classes (tests/fuzz_configs.py: 2-8 stages,
+    random trees, capacities 5-450 (uint8 and int16 state), delays 1-5, horizons 10-50, raw or
+    standardised actions, shared rewards for the multi-agent classes, explicit order_max), in-kernel
+    Poisson / uniform demand, noisy demand on trees, noisy delay; float32 or float64 plans drawn around
+    the action range (standardised: beyond [a, b]; raw: beyond [0, order_max], fractional). Every
+    per-episode value and per-step reward equals the oracle."""
+    got, ref, _ = drawn_plan_case(9090 + i, i)
+    for k in STATS + ("rewards",):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
