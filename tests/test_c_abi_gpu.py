@@ -53,3 +53,37 @@ def test_cpp_host_reproduces_reference_golden(name, tmp_path):
     assert lines[0].split() == ["0"] * (T - 1) + ["1"]
     assert lines[1] == "past_horizon_rc %d" % nat.E_DONE
     assert lines[2].startswith("jit:imenv_step_jit["), lines[2]
+
+
+PLAN_BIN = os.path.join(ROOT, "examples", "bin", "c_abi_plan")
+
+
+@pytest.mark.parametrize("name", ["SHLP8", "SHLP_div1", "SHLP_div2"])
+def test_cpp_host_plan_replay_reproduces_reference_golden(name, tmp_path):
+    """examples/c_abi_plan.cpp: one imenv_plan_rollout call from C++ replays every scenario's own plan
+    and returns the LP scripts' per-step rewards and sums, equal to the reference loop's bit for bit."""
+    from golden_io import load_base_stock
+    from imenv import build_spec
+    if not os.path.exists(PLAN_BIN):
+        pytest.fail("examples/bin/c_abi_plan not built (python __graft_entry__.py build)")
+    meta, cases = load_base_stock("plan_replay.npz")
+    m, d = meta[name], cases[name]
+    assert m["layout"] == "episode" and d["plans"].shape[1] == 1
+    spec = build_spec(m["kind"], m["config"]).to_c()
+    T, _, S, N = d["plans"].shape
+    dem = d["demand"] if d["demand"].ndim == 3 else d["demand"][:, None, :]     # [S, R, T]
+    R = dem.shape[1]
+    (tmp_path / "spec.bin").write_bytes(ctypes.string_at(ctypes.addressof(spec), ctypes.sizeof(spec)))
+    (tmp_path / "dims.txt").write_text("%d %d %d %d\n" % (S, T, N, R))
+    np.ascontiguousarray(dem.transpose(2, 1, 0), dtype=np.int32).tofile(tmp_path / "demand.i32")
+    np.ascontiguousarray(d["plans"][:, 0], dtype=np.float64).tofile(tmp_path / "plans.f64")
+    r = subprocess.run([PLAN_BIN, str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    rew = np.fromfile(tmp_path / "rewards.f64").reshape(T, S)
+    st = np.fromfile(tmp_path / "stats.f64").reshape(5, S)
+    np.testing.assert_array_equal(rew, d["rewards"][:, 0])
+    for j, k in ((0, "return"), (2, "inventory"), (3, "backlog"), (4, "customer_backlog")):
+        np.testing.assert_array_equal(st[j], d[k][0], err_msg=k)
+    ms = np.fromfile(tmp_path / "mean_std.f64").reshape(5, 2)
+    np.testing.assert_allclose(ms[0], [np.mean(d["return"][0]), np.std(d["return"][0])], rtol=1e-12)
+    assert "rollout jit:imenv_rollout_jit[" in (tmp_path / "info.txt").read_text()
