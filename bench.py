@@ -1,28 +1,38 @@
 #!/usr/bin/env python3
 """Throughput bench for the north-star path: env-steps/s of the HIP step kernel.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n-envs E] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4] [--n-envs E]
+                    [--gather] [--no-cpu-baseline]
 
 Workload (BASELINE.json metric "env-steps/sec (whole node), 4-stage x 2^20 envs"):
 MultiAgentInvManagement, 4 stages, MA_1 flags (hyperparams.py:344; constants
 inv_management.py:35-56), shared reward, 2^20 envs per GPU, 30-period episodes,
 in-kernel Philox Poisson(5) demand, float32 actions pre-generated [30][n][4]
 (torch.Generator seed 0) and float32 observations written into a [30][n][4][3]
-rollout buffer, float64 rewards. A "step" = one step() of every env; the reset
-at each episode boundary runs inside the timed region. Multi-GPU: one process
-per GPU (torchrun), each rank owns 2^20 envs at env_offset rank*2^20 (weak
-scaling, no data-path collective; --gather adds the optional per-step RCCL
-all-gather of obs+reward, reported separately).
+rollout buffer, float64 rewards. A "step" = one step() of every env; the reset kernel
+runs at each episode boundary, and the line's "resets_timed" says how many of them
+fell inside the timed region.
 
-Prints ONE JSON line on rank 0 (keys per the driver contract), with
-"roofline" (step kernel: algorithmic bytes / HIP-event-timed kernel duration vs
-8 TB/s) and "cpu_baseline" (the oracle port, one env per process, timed on this
-box's host cores before the GPU is touched).
+Multi-GPU: one process per GPU, each rank owns 2^20 envs at env_offset rank*2^20 (weak
+scaling, no data-path collective). The ranks come either from an external launcher
+(torchrun sets WORLD_SIZE / RANK / LOCAL_RANK) or, for `--gpus N` with no launcher, from
+this script itself: the parent process starts N rank processes before it (or they) touch
+the GPU, and exits with the first non-zero rank status. `--gather` adds the optional
+per-step RCCL all-gather of obs+reward; its own time is reported apart from the kernel's.
+The reference's own parallelism is one env per RLlib worker process (hyperparams.py:14,
+MA_inv_management.py:172); the rank processes replace those workers.
+
+Prints ONE JSON line on rank 0 (keys per the driver contract), with "roofline" (step
+kernel: algorithmic bytes / HIP-event-timed kernel duration vs 8 TB/s; plus an
+informational HIP-graph-replayed episode) and "cpu_baseline" (the oracle port, one env
+per process, timed on this box's host cores before the GPU is touched).
 """
 import argparse
 import json
 import multiprocessing as mp
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,6 +46,7 @@ import numpy as np  # noqa: E402
 METRIC = "env-steps/sec (whole node), 4-stage × 2^20 envs; % HBM roofline"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E (spec)
 CPU_SHARE = 16             # host cores per GPU on the GPU box (worker pools must stay within it)
+CPU_BASELINE_ENV = "IMENV_BENCH_CPU_BASELINE"   # launcher -> rank 0: the CPU baseline it measured
 
 C2_CONFIG = dict(num_stages=4, num_periods=30, init_inv=np.ones(4) * 10, inv_target=np.zeros(4),
                  inv_max=np.ones(4) * 30, price=np.array([5, 4, 3, 2, 1]),
@@ -93,8 +104,9 @@ def cpu_baseline(seconds=1.5, cname="C2"):
     """Oracle port of the reference step(), one env per process (the reference's own usage:
     one env per RLlib worker), a pool over this box's cores. Runs in a child interpreter
     started with BLAS threads pinned to 1 (they must be set before numpy is imported)."""
-    import subprocess
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-only", "--cpu-seconds", str(seconds),
                         "--config", cname],
                        env=env, capture_output=True, text=True, timeout=600)
@@ -123,18 +135,101 @@ def _cpu_baseline_here(seconds, cname):
 
 # ----------------------------------------------------------------- PMC traffic
 def pmc_traffic(n_envs, kernel):
-    """HBM bytes per step-kernel launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_step_kernel.json, written by tools/profile_pmc.sh -> tools/pmc_summary.py for
-    this workload), else None. Only a summary of this exact kernel variant (kernel_info) counts."""
-    p = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
-    try:
-        with open(p) as f:
-            d = json.load(f)
-        if int(d.get("n_envs", -1)) == int(n_envs) and d.get("kernel_info") == kernel:
-            return float(d["hbm_bytes_per_launch"])
-    except Exception:
-        pass
+    """HBM bytes per step-kernel launch from a committed rocprofv3 PMC summary of this exact kernel
+    variant (kernel_info) at this size: profiles/pmc_step_kernel.json (the metric's workload, written by
+    tools/profile_pmc.sh) or profiles/pmc_configs/*.json (the C3 / C4 configs, tools/profile_configs.sh),
+    else None."""
+    import glob
+    paths = [os.path.join(ROOT, "profiles", "pmc_step_kernel.json")]
+    paths += sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_configs", "*.json")))
+    for p in paths:
+        try:
+            with open(p) as f:
+                d = json.load(f)
+            if int(d.get("n_envs", -1)) == int(n_envs) and d.get("kernel_info") == kernel:
+                return float(d["hbm_bytes_per_launch"])
+        except Exception:
+            continue
     return None
+
+
+# ----------------------------------------------------------------- launcher
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv):
+    """`--gpus N` (N > 1) with no launcher: start N rank processes of this script, one per GPU, from a
+    process that has not touched the GPU (no exec: children, whose exit codes this one returns). Rank 0
+    prints the line. The CPU baseline runs here first, on the host cores, and is handed to rank 0."""
+    n = args.gpus
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds, args.config)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, WORLD_SIZE=str(n), RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), IMENV_BENCH_LAUNCHER="self")
+        if cpu is not None:
+            env[CPU_BASELINE_ENV] = json.dumps(cpu)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        time.sleep(0.05)
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                sys.stderr.write("bench.py: rank process %d exited with %d; stopping the others\n" % (p.pid, code))
+                for q in alive:
+                    q.terminate()
+    sys.exit(rc)
+
+
+def ranks_census(dist, dev):
+    """Every rank's (rank, local rank, device, PCI bus id): the line reports how many distinct ranks and
+    GPUs took part, so a line cannot claim N GPUs while fewer ran."""
+    import torch
+    me = {"rank": dist.get_rank() if dist.is_initialized() else 0,
+          "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "host": socket.gethostname()}
+    if dev is not None:
+        pr = torch.cuda.get_device_properties(dev)
+        me.update(device=dev.index, gpu="%04x:%02x:%02x" % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id))
+    if not dist.is_initialized():
+        return [me]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, me)
+    return out
+
+
+def dry_run(args, world, rank):
+    """The launcher / rendezvous / census / max-reduction path with no GPU work (CPU tests, gloo): the
+    line carries n_gpus and ranks_seen, value null."""
+    import torch
+    import torch.distributed as dist
+    if os.environ.get("IMENV_BENCH_DRY_FAIL_RANK") == str(rank):     # tests: a rank that dies
+        sys.exit(7)
+    if world > 1:
+        dist.init_process_group("gloo")
+    census = ranks_census(dist, None)
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "env-steps/s", "n_gpus": world,
+                          "dry_run": True, "ranks_seen": len({c["rank"] for c in census}), "ranks": census,
+                          "max_over_ranks": t.item(), "launcher": os.environ.get("IMENV_BENCH_LAUNCHER", "external"),
+                          "cpu_baseline": json.loads(os.environ[CPU_BASELINE_ENV])
+                          if CPU_BASELINE_ENV in os.environ else None}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 # ----------------------------------------------------------------- main
@@ -150,26 +245,46 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--gather", action="store_true", help="add the per-step RCCL all-gather of obs+reward")
-    ap.add_argument("--store", default="default", choices=["default", "stream"],
-                    help="observation / reward store policy of the step kernel (imenv_set_store_policy)")
+    ap.add_argument("--store", default="default", choices=["default", "stream", "plain", "writethrough"],
+                    help="store policy of the step kernel (imenv_set_store_policy)")
     ap.add_argument("--no-alt-store", action="store_true", help="skip the informational run of the other policy")
+    ap.add_argument("--no-graph", action="store_true", help="skip the informational HIP-graph episode replay")
     ap.add_argument("--cpu-only", action="store_true", help=argparse.SUPPRESS)
     # rehearsal of the multi-rank path on a one-GPU box: every rank on device 0, gloo for the
     # barrier / max-reduction (the driver's N-GPU runs use one GPU per rank and RCCL)
     ap.add_argument("--rehearse-one-gpu", action="store_true", help=argparse.SUPPRESS)
-    args = ap.parse_args()
+    # launcher / rendezvous / census path only, no GPU work (CPU tests)
+    ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
+    if args.steps < 1 or args.warmup < 0 or args.gpus < 1:
+        ap.error("--steps must be >= 1, --warmup >= 0, --gpus >= 1")
     if args.cpu_only:
         print(json.dumps(_cpu_baseline_here(args.cpu_seconds, args.config)))
         return
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        launch_ranks(args, argv)          # never returns
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.stderr.write("bench.py: --gpus %d but the launcher started %d ranks\n" % (args.gpus, world))
+        sys.exit(2)
+    if args.dry_run:
+        dry_run(args, world, rank)
+        return
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds, args.config)          # before the GPU is initialised
+    if rank == 0 and not args.no_cpu_baseline:
+        if CPU_BASELINE_ENV in os.environ:      # measured by this script's own launcher before the ranks started
+            cpu = json.loads(os.environ[CPU_BASELINE_ENV])
+        else:
+            cpu = cpu_baseline(args.cpu_seconds, args.config)          # before the GPU is initialised
 
+    if args.gather and world > 1 and not args.rehearse_one_gpu:
+        # RCCL records start / end events around every collective on its own stream (Work._get_duration)
+        os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")
     import torch
     import torch.distributed as dist
     from imenv import VectorInvEnv
@@ -185,6 +300,12 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+    census = ranks_census(dist, dev)
+    ranks_seen = len({c["rank"] for c in census})
+    gpus_seen = len({(c["host"], c["gpu"]) for c in census})
+    if ranks_seen != world:
+        sys.stderr.write("bench.py: %d ranks took part, world size is %d\n" % (ranks_seen, world))
+        sys.exit(3)
 
     kind, ccfg, cdesc, cn = CONFIGS[args.config]
     n = args.n_envs or cn
@@ -207,6 +328,10 @@ def main():
     o_ptr = [obs_buf[t].data_ptr() for t in range(T)]
     r_ptr = [rew_buf[t].data_ptr() for t in range(T)]
 
+    def reset(sp):
+        nat.check(lib.imenv_reset(h, None, nat.LAYOUT_DRAW, 0, 0.0, None, -1, obs0.data_ptr(), nat.F32, sp),
+                  "imenv_reset")
+
     # HIP events on the kernel's own stream bracket every run of consecutive step launches between two
     # resets (at most one episode, and the part of one that the timed region holds): per-launch
     # duration = elapsed / launches of the run, back-to-back dispatch gaps included, the reset kernel
@@ -214,13 +339,15 @@ def main():
     # pair per episode: a pair per step would cost ~7 us of GPU time each and slow the very loop
     # being measured (tools/launch_probe.py).
     def run(first, steps, events=None):
-        """Steps first .. first+steps-1 of the bench's step sequence (period t = step mod T)."""
+        """Steps first .. first+steps-1 of the bench's step sequence (period t = step mod T). Returns
+        the number of resets it ran."""
         pair = None
+        resets = 0
         for s in range(first, first + steps):
             t = s % T
             if t == 0:
-                nat.check(lib.imenv_reset(h, None, nat.LAYOUT_DRAW, 0, 0.0, None, -1, obs0.data_ptr(), nat.F32,
-                                          sptr), "imenv_reset")
+                reset(sptr)
+                resets += 1
             if events is not None and pair is None:
                 pair = [pool.pop(), pool.pop(), []]     # pre-created in timed()
                 pair[0].record(stream)
@@ -245,13 +372,15 @@ def main():
                     gather.result(s - 1)     # the learner's view of step s-1: [world*n, N, F], [world*n]
         if gather is not None and steps:
             gather.result(first + steps - 1)
+        return resets
 
     per_t = env.step_traffic_per_period()
 
     def timed(W, K):
         """W untimed warmup steps (the first one resets), then exactly K timed steps of the same step
         sequence, so the timed region holds the resets at its episode boundaries. Returns (wall s,
-        kernel ms per launch, algorithmic bytes per timed launch), max over ranks."""
+        kernel ms per launch, algorithmic bytes per timed launch, timed launches, resets timed), max
+        over ranks."""
         if W == 0:
             run(0, 1)     # no warmup asked for: one step outside the sequence builds the hipRTC kernel
         run(0, W)
@@ -262,11 +391,13 @@ def main():
             e.record(stream)
         torch.cuda.synchronize(dev)
         events = []
+        if gather is not None:
+            gather.keep_works(True)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        run(W, K, events)
+        resets = run(W, K, events)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -278,25 +409,35 @@ def main():
             tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             el, kern_ms = tt[0].item(), tt[1].item()
-        return el, kern_ms, bpl, sum(len(ts) for _, _, ts in events)
+        return el, kern_ms, bpl, sum(len(ts) for _, _, ts in events), resets
 
     pool = []
     W, K = args.warmup, args.steps
     env.set_store_policy(args.store)
-    el, kern_ms, bytes_per_launch, launches = timed(W, K)
-    kinfo = env.kernel_info()          # the timed kernel (before the informational run below)
+    el, kern_ms, bytes_per_launch, launches, resets_timed = timed(W, K)
+    kinfo = env.kernel_info()          # the timed kernel (before the informational runs below)
+
+    gather_info = None
+    if gather is not None:
+        gather_info = gather_report(gather, dist, dev, stream, K, world, n)
+
     alt = None
     if world == 1 and not args.no_alt_store:
-        # the other store policy on the same handle (informational; the line's value is args.store's)
-        other = "stream" if args.store == "default" else "default"
+        # another store policy on the same handle (informational; the line's value is args.store's):
+        # plain cached stores (round 2's default) next to the default, else the default
+        other = "plain" if args.store == "default" else "default"
         env.set_store_policy(other)
-        a_el, a_kern, a_bpl, _ = timed(W, K)
+        a_el, a_kern, a_bpl, _, _ = timed(W, K)
         a_kinfo = env.kernel_info()
         env.set_store_policy(args.store)
         alt = {"store_policy": other, "kernel": a_kinfo, "value": round(n * K / a_el, 1),
                "ms_per_step": round(a_el / K * 1e3, 6),
                "kernel_us": round(a_kern * 1e3, 3), "achieved": round(a_bpl / (a_kern * 1e-3) / 1e9, 1),
                "frac": round(a_bpl / (a_kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+    graph = None
+    if world == 1 and gather is None and not args.no_graph:
+        graph = graph_episode_run(torch, env, reset, lib, nat, a_ptr, o_ptr, r_ptr, per_t, n, T, dev)
 
     # measured stream-copy ceiling at the step's byte count: a device copy of half the
     # bytes moves them once in and once out; outside the timed region
@@ -320,6 +461,7 @@ def main():
     es = env.state_layout()[0]
     achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic = pmc_traffic(n, kinfo)
+    launcher = os.environ.get("IMENV_BENCH_LAUNCHER", "external" if world > 1 else "none")
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -333,13 +475,20 @@ def main():
         "vs_baseline": None,
         "dtype": "%s state, f64 reward, f32 obs/actions" % {1: "u8", 2: "int16", 4: "int32"}[es],
         "data": "synthetic: in-kernel Philox4x32-10 Poisson(5) demand, uniform[-1,1] f32 actions (torch seed 0)",
+        "ranks_seen": ranks_seen,
+        "gpus_seen": gpus_seen if not args.rehearse_one_gpu else 1,
+        "launcher": launcher,
+        "resets_timed": resets_timed,
         "config": {
-            "workload": "%s%s: %s, %s envs per GPU, 30-period episodes with the reset inside the timed loop"
+            "workload": "%s%s: %s, %s envs per GPU, 30-period episodes; %d timed steps, %d of them "
+                        "preceded by the episode's reset kernel inside the timed region"
                         % (args.config, " shape at the metric's size" if args.config == "C2" else "", cdesc,
-                           "2^20" if n == 1 << 20 else str(n)),
+                           "2^20" if n == 1 << 20 else str(n), K, resets_timed),
             "n_envs_per_gpu": n, "global_envs": world * n, "num_stages": N, "obs_features": F,
-            "num_periods": T, "parallelism": "env-sharded x%d (one process per GPU, no data-path collective%s)"
-                                             % (world, ", + RCCL all-gather of obs/reward per step" if gather is not None else ""),
+            "num_periods": T,
+            "parallelism": "env-sharded x%d (one process per GPU%s, no data-path collective%s)"
+                           % (world, ", all on GPU 0 with gloo: rehearsal" if args.rehearse_one_gpu else "",
+                              ", + RCCL all-gather of obs/reward per step" if gather is not None else ""),
         },
         "roofline": {
             "bound": "hbm",
@@ -358,7 +507,9 @@ def main():
             "bytes_per_launch": round(bytes_per_launch),
             "store_policy": args.store,
             "alt_store_policy": alt,
+            "graph": graph,
         },
+        "gather": gather_info,
         "cpu_baseline": cpu,
     }
     if cpu:
@@ -368,6 +519,89 @@ def main():
     env.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def gather_report(gather, dist, dev, stream, K, world, n):
+    """The per-step all-gather's own time, apart from the kernel's: (1) RCCL's start / end events on its
+    own stream for each collective of the timed region (Work._get_duration, TORCH_NCCL_ENABLE_TIMING),
+    mean and max over ranks; (2) the same collective timed alone, K back to back, with events on the
+    current stream (which waits on RCCL's stream after each). Bytes are the packed send buffer."""
+    import torch
+    works = gather.keep_works(False)
+    in_loop = None
+    try:
+        d = [w._get_duration() for w in works]
+        if d and all(x is not None and x >= 0 for x in d):
+            in_loop = sum(d) / len(d)
+    except Exception:
+        in_loop = None
+    # alone: K collectives of buffer 0, nothing else on the GPU
+    reps = max(5, min(K, 50))
+    gather.start(0)
+    gather.wait(0)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        gather.start(0)
+        gather.wait(0)
+    e1.record(stream)
+    e1.synchronize()
+    alone = e0.elapsed_time(e1) / reps
+    t = torch.tensor([in_loop if in_loop is not None else -1.0, alone], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    in_loop_max = t[0].item() if in_loop is not None else None
+    recv = gather.chunk * world
+    return {
+        "collective": "all_gather_into_tensor" if gather._into else "all_gather (gloo)",
+        "send_bytes_per_rank": gather.chunk, "recv_bytes_per_rank": recv,
+        "gather_us": round(in_loop_max * 1e3, 3) if in_loop_max is not None else None,
+        "gather_us_source": "RCCL stream events per timed collective (max over ranks of the mean)"
+                            if in_loop_max is not None else "unavailable",
+        "gather_alone_us": round(t[1].item() * 1e3, 3),
+        "gather_alone_recv_gbs": round(recv / (t[1].item() * 1e-3) / 1e9, 1),
+        "collectives_timed": len(works),
+    }
+
+
+def graph_episode_run(torch, env, reset, lib, nat, a_ptr, o_ptr, r_ptr, per_t, n, T, dev, replays=10):
+    """Informational: one episode (reset + T steps) captured into a HIP graph and replayed back to back
+    (the host out of the loop: a trainer that captures its sampler). Each replay draws the next episode's
+    demand (the reset kernel advances the device episode counter). ms_per_step and value count the reset
+    with its episode."""
+    s = torch.cuda.Stream(dev)
+    graph = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize(dev)
+    with torch.cuda.graph(graph, stream=s):
+        sp = torch.cuda.current_stream(dev).cuda_stream
+        reset(sp)
+        for t in range(T):
+            rc = lib.imenv_step(env._h, a_ptr[t], nat.F32, o_ptr[t], nat.F32, r_ptr[t], None, None, sp)
+            if rc:
+                nat.check(rc, "imenv_step")
+    kinfo = env.kernel_info()
+    cur = torch.cuda.current_stream(dev)
+    graph.replay()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(cur)
+    for _ in range(replays):
+        graph.replay()
+    e1.record(cur)
+    e1.synchronize()
+    wall = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1)
+    steps = replays * T
+    bytes_ep = sum(per_t[t] for t in range(T)) * n
+    del graph
+    return {"kernel": kinfo, "replays": replays, "steps": steps, "ms_per_step": round(ms / steps, 6),
+            "value": round(n * steps / (ms * 1e-3), 1), "host_wall_ms_per_step": round(wall * 1e3 / steps, 6),
+            "achieved_incl_reset": round(bytes_ep * replays / (ms * 1e-3) / 1e9, 1),
+            "frac_incl_reset": round(bytes_ep * replays / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 if __name__ == "__main__":

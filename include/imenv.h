@@ -376,14 +376,21 @@ int imenv_set_delay_uniforms(ImEnv* env, int32_t period, const double* u, void* 
  * IMENV_E_UNSUPPORTED from step()); set_jit(1) retries failed combinations. */
 int imenv_set_jit(ImEnv* env, int mode);
 
-/* Store policy of the step kernel's observation and reward stores (hipRTC kernels; the ahead-of-time
- * kernels always use the default). IMENV_STORE_DEFAULT: plain stores, the lines stay cache-resident
- * for a consumer that reads them right after the step (a policy forward). IMENV_STORE_STREAM:
- * non-temporal stores, for outputs that go to a rollout buffer read later: the step runs 4-17%
- * faster, a consumer reading them at once pays more than that. Results identical.
- * No reference counterpart (a performance knob of this implementation). */
+/* Store policy of the step kernel's output stores (hipRTC kernels; the ahead-of-time kernels always
+ * use plain stores). Results are identical under every policy; no reference counterpart (a
+ * performance knob of this implementation).
+ *  IMENV_STORE_DEFAULT: observation and reward stores write-through (cache policy sc1: written to
+ *    memory at once, nothing left dirty in L2 for the end-of-launch write-back, which otherwise
+ *    costs ~bytes / 6 TB/s at every dependent launch boundary); the state rows too when a launch's
+ *    observation + reward bytes fit the 32 MiB of L2 (small batches), else plain.
+ *  IMENV_STORE_STREAM: non-temporal observation / reward stores (outputs bound for a rollout buffer
+ *    read much later).
+ *  IMENV_STORE_PLAIN: plain cached stores everywhere (the round-2 default).
+ *  IMENV_STORE_WRITETHROUGH: write-through for observations, rewards and state rows at any size. */
 #define IMENV_STORE_DEFAULT 0
 #define IMENV_STORE_STREAM 1
+#define IMENV_STORE_PLAIN 2
+#define IMENV_STORE_WRITETHROUGH 3
 int imenv_set_store_policy(ImEnv* env, int policy);
 
 /* NUL-terminated description of the kernel the last step() launched, truncated to len bytes. */
@@ -392,12 +399,20 @@ int imenv_kernel_info(const ImEnv* env, char* buf, int64_t len);
 /* Diagnostics (no device needed): generate and compile with hipRTC the specialised step kernel of
  * `spec` for `arch` (e.g. "gfx950"); flags = bit0 f64 actions, bit1 f64 obs, bit2 noisy delay,
  * bit3 noisy demand, bit4 host-fed delay uniforms, bits 5-9 demand layout, bit10 episode metrics, bit11
- * streaming stores (IMENV_STORE_STREAM). With bit 12 set it
+ * streaming stores (IMENV_STORE_STREAM), bit13 write-through observation / reward stores, bit14
+ * write-through state rows. With bit 12 set it
  * compiles the rollout kernel instead: bit13 demand table, bit14 noisy delay, bit15 noisy
  * demand, bit16 objective, bits 17-18 action source (0 base-stock, 1 shared plan, 2 per-episode
  * plan), bit19 float64 plan actions. `log` receives "ok" or
  * the compiler log. */
 int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, char* log, int64_t log_len);
+
+/* Diagnostics: per-wave phase timestamps of the last step() launched by a kernel built with
+ * -DIMENV_STAMPS=1 (IMENV_JIT_OPTS) on a handle created with IMENV_STAMPS=1 in the environment:
+ * 8 uint64 per wave (s_memrealtime, 100 MHz: entry, loads issued, loads landed, computed, slab
+ * barrier passed, stores issued, stores acknowledged; then XCC id << 32 | block). Copies up to cap
+ * values to HOST memory (synchronous); *count receives the buffer length (0: no stamps). */
+int imenv_debug_stamps(ImEnv* env, uint64_t* out, int64_t cap, int64_t* count);
 
 void imenv_destroy(ImEnv* env);
 

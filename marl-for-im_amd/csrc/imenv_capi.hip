@@ -366,6 +366,7 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 uint64_t prob_thr32(double p) {
+  if (!(p > 0.0)) return 0;   // also NaN: the reference's `uniform() < nan` is never true
   double v = std::ceil(p * 4294967296.0);
   if (v < 0) v = 0;
   if (v > 4294967296.0) v = 4294967296.0;
@@ -550,17 +551,36 @@ int validate_and_derive(const ImEnvSpec& s, SpecDev& d, int& maxc) {
   if (s.reward_mode < IMENV_REWARD_SUM || s.reward_mode > IMENV_REWARD_INDEPENDENT)
     return fail(IMENV_E_INVALID, "bad reward_mode");
   if (s.standardise_actions && !(s.b - s.a != 0.0)) return fail(IMENV_E_INVALID, "a == b");
+  // the reference's numbers are finite (MAIM_env.py:166-168 asserts the price order, which no NaN
+  // passes); a non-finite price / cost / scale would only turn rewards or observations into NaN
+  if (!std::isfinite(s.a) || !std::isfinite(s.b)) return fail(IMENV_E_INVALID, "a and b must be finite");
+  for (int i = 0; i < N; ++i) {
+    if (!std::isfinite(s.sell_price[i]) || !std::isfinite(s.buy_price[i]) || !std::isfinite(s.stock_cost[i]) ||
+        !std::isfinite(s.backlog_cost[i]) || !std::isfinite(s.inv_target[i]))
+      return fail(IMENV_E_INVALID, "prices, costs and inventory targets must be finite");
+    for (int q = 0; q < 4; ++q)
+      if (s.split_limit[i][q] < 0) return fail(IMENV_E_INVALID, "split guard limits must be >= 0");
+  }
+  for (int g = 0; g < IMENV_NUM_GROUPS; ++g) {
+    if (s.group_mode[g] != IMENV_OBS_SCALED && s.group_mode[g] != IMENV_OBS_CLAMP_SCALED) continue;
+    for (int i = 0; i < N; ++i) {
+      if (std::isnan(s.group_den[g][i])) return fail(IMENV_E_INVALID, "observation denominator is NaN");
+      if (s.group_mode[g] == IMENV_OBS_CLAMP_SCALED && !(s.group_clip[g][i] >= 0.0 && std::isfinite(s.group_clip[g][i])))
+        return fail(IMENV_E_INVALID, "observation clamp must be finite and >= 0");
+    }
+  }
   d.table_len = 0;
   if (s.demand_dist == IMENV_DEMAND_POISSON) {
     // thr[k] = ceil(CDF(k) * 2^32) by the pmf recurrence (oracle/philox.py:poisson_thresholds)
     const double mu = s.poisson_mu;
-    if (!(mu > 0.0)) return fail(IMENV_E_INVALID, "Poisson mean must be positive");
+    if (!(mu > 0.0) || !std::isfinite(mu)) return fail(IMENV_E_INVALID, "Poisson mean must be positive and finite");
     double p = std::exp(-mu), cdf = 0.0;
     int k = 0;
     for (;;) {
       cdf += p;
       const double tv = std::ceil(cdf * 4294967296.0);
       if (tv >= 4294967296.0) break;
+      if (!(tv >= 0.0)) return fail(IMENV_E_INVALID, "Poisson table: non-finite probability");
       if (k >= IMENV_TABLE_MAX) return fail(IMENV_E_UNSUPPORTED, "Poisson mean too large for the inversion table");
       d.table[k] = (uint32_t)tv;
       ++k;
@@ -600,6 +620,26 @@ int alloc(T** p, size_t count) {
   if (count == 0) { *p = nullptr; return IMENV_OK; }
   HIPCHK(hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)));
   return IMENV_OK;
+}
+
+// IMENV_STORE_DEFAULT: the state rows are written through as well when a launch's observation and
+// reward bytes fit the 32 MiB of L2 (8 XCDs x 4 MiB): then nearly every line a launch writes would
+// still be dirty at its end and the dependent-launch boundary would write it back (+ bytes / 6 TB/s,
+// MI355X_MICROARCH.md); larger launches evict their lines during the launch anyway, and there a state
+// row written through (a 64-byte ring row per wave: partial lines) costs more than it saves
+// (profiles/r03/).
+// IMENV_WT_STATE_MAX_BYTES overrides the 32 MiB limit (read once; tuning sweeps).
+int64_t wt_state_limit() {
+  static const int64_t lim = [] {
+    const char* v = std::getenv("IMENV_WT_STATE_MAX_BYTES");
+    return v ? (int64_t)std::atoll(v) : (int64_t(32) << 20);
+  }();
+  return lim;
+}
+bool wt_state_pays(const ImEnvSpec& s, int64_t n, bool obs_f64) {
+  const int64_t per_env = (int64_t)s.num_nodes * s.num_features * (obs_f64 ? 8 : 4) +
+                          (s.reward_mode == IMENV_REWARD_INDEPENDENT ? 8 * s.num_nodes : 8);
+  return n * per_env <= wt_state_limit();
 }
 
 bool is_base_obs(const ImEnvSpec& s) {
@@ -650,6 +690,8 @@ struct ImEnv {
   size_t roll_terms_cap = 0;
   std::string last_rollout;
   double* d_metrics = nullptr;   // caller-owned [n][4 + N] (imenv_set_episode_metrics)
+  uint64_t* d_stamps = nullptr;  // diagnostics: per-wave phase stamps of IMENV_STAMPS kernel builds
+  int64_t n_stamps = 0;
 };
 
 extern "C" {
@@ -665,7 +707,7 @@ void imenv_destroy(ImEnv* h) {
   (void)hipSetDevice(h->device);
   void* ptrs[] = {h->d_spec, h->d_net, h->d_ou, h->d_ring, h->d_carry, h->d_bto, h->d_hist_d,
                   h->d_hist_o, h->d_demand, h->d_delay_u, h->d_err, h->d_err_any, h->d_lut32, h->d_lut64,
-                  h->d_episode, h->d_roll_part, h->d_roll_terms};
+                  h->d_episode, h->d_roll_part, h->d_roll_terms, h->d_stamps};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& kv : h->jit_k)
@@ -733,6 +775,13 @@ int imenv_create(const ImEnvSpec* spec, int64_t n_envs, int64_t env_offset, int 
   if (h->arch.empty()) h->jit = 0;
   if (const char* v = std::getenv("IMENV_JIT")) h->jit = (std::atoi(v) != 0 && !h->arch.empty()) ? 1 : 0;
   if (const char* v = std::getenv("IMENV_JIT_STRICT")) h->jit_strict = std::atoi(v) != 0;
+  if (const char* v = std::getenv("IMENV_STAMPS")) {   // diagnostics (imenv_debug_stamps)
+    if (std::atoi(v) != 0) {
+      h->n_stamps = ((int64_t)n + 63) / 64 * 8 + 64 * 8;   // 8 per wave (+ a block's tail waves)
+      if ((rc = alloc(&h->d_stamps, (size_t)h->n_stamps)) != IMENV_OK) { imenv_destroy(h); return rc; }
+      (void)hipMemset(h->d_stamps, 0, (size_t)h->n_stamps * sizeof(uint64_t));
+    }
+  }
   *out = h;
   return IMENV_OK;
 }
@@ -817,6 +866,7 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
   A.lut64 = h->d_lut64;
   A.episode = h->d_episode;
   A.metrics = h->d_metrics;
+  A.stamps = h->d_stamps;
   A.n = h->n;
   A.env_offset = (uint32_t)h->env_offset;
   A.t = h->t;
@@ -846,6 +896,9 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
     f.demand_layout = A.demand_layout;
     f.metrics = A.metrics != nullptr;
     f.stream_store = h->store_policy == IMENV_STORE_STREAM;
+    f.wt_obs = h->store_policy == IMENV_STORE_DEFAULT || h->store_policy == IMENV_STORE_WRITETHROUGH;
+    f.wt_state = h->store_policy == IMENV_STORE_WRITETHROUGH ||
+                 (h->store_policy == IMENV_STORE_DEFAULT && wt_state_pays(s, h->n, A.obs_f64 != 0));
     auto it = h->jit_k.find(f.key());
     if (it == h->jit_k.end()) {
       // compiling + loading a module is not stream work: never do it while the stream is being
@@ -1264,8 +1317,8 @@ int imenv_set_delay_uniforms(ImEnv* h, int32_t period, const double* u, void* st
 
 int imenv_set_store_policy(ImEnv* h, int policy) {
   if (!h) return fail(IMENV_E_INVALID, "null handle");
-  if (policy != IMENV_STORE_DEFAULT && policy != IMENV_STORE_STREAM)
-    return fail(IMENV_E_INVALID, "policy must be IMENV_STORE_DEFAULT or IMENV_STORE_STREAM");
+  if (policy < IMENV_STORE_DEFAULT || policy > IMENV_STORE_WRITETHROUGH)
+    return fail(IMENV_E_INVALID, "policy must be one of IMENV_STORE_DEFAULT / STREAM / PLAIN / WRITETHROUGH");
   h->store_policy = policy;
   return IMENV_OK;
 }
@@ -1292,6 +1345,16 @@ int imenv_kernel_info(const ImEnv* h, char* buf, int64_t len) {
   return IMENV_OK;
 }
 
+int imenv_debug_stamps(ImEnv* h, uint64_t* out, int64_t cap, int64_t* count) {
+  if (!h || !count) return fail(IMENV_E_INVALID, "null argument");
+  *count = h->n_stamps;
+  if (!h->d_stamps || !out || cap <= 0) return IMENV_OK;
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out, h->d_stamps, (size_t)std::min(cap, h->n_stamps) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return IMENV_OK;
+}
+
 int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, char* log, int64_t log_len) {
   if (!spec || !arch) return fail(IMENV_E_INVALID, "null argument");
   SpecDev d;
@@ -1310,6 +1373,8 @@ int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, cha
   f.has_delay_u = flags & 16u;
   f.metrics = flags & 1024u;
   f.stream_store = flags & 2048u;
+  f.wt_obs = flags & 8192u;
+  f.wt_state = flags & 16384u;
   f.demand_layout = (int)((flags >> 5) & 31u);
   std::string msg;
   std::string src;

@@ -56,6 +56,15 @@ typedef unsigned long long uint64_t;
 #ifndef IMENV_WAVE_SLAB
 #define IMENV_WAVE_SLAB 0    // 1: each wave writes out its own staged observation rows (step_body)
 #endif
+#ifndef IMENV_WT_STORE
+#define IMENV_WT_STORE 0     // 1: observation / reward stores of the step kernel are write-through (sc1)
+#endif
+#ifndef IMENV_WT_STATE
+#define IMENV_WT_STATE 0     // 1: the step kernel's state-row stores are write-through (sc1)
+#endif
+#ifndef IMENV_STAMPS
+#define IMENV_STAMPS 0       // 1 (diagnostic builds only): per-wave phase timestamps into StepArgs::stamps
+#endif
 #define IMENV_GUIDE_BITS 10
 
 namespace imenv {
@@ -71,6 +80,35 @@ __device__ __forceinline__ void store16(V* p, const V& v) {
   } else {
     *p = v;
   }
+}
+
+// Write-through stores (cache policy sc1): the line is written to memory at once and dropped from
+// the XCD's L2 (MI355X_MICROARCH.md, "stores of each flavour"), so a launch leaves no dirty lines for
+// the end-of-kernel write-back (the dependent-boundary cost "+ B / 6 TB/s") and its HBM writes overlap
+// the rest of the launch. Raw buffer stores carry the policy bits; the resource's base is wave-uniform
+// (a block's slab), the per-lane part is the 32-bit byte offset.
+constexpr int CPOL_SC1 = 16;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
+}
+template <typename V>
+__device__ __forceinline__ void wt_store16(__amdgpu_buffer_rsrc_t r, int off, const V& v) {
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  u4 w;
+  __builtin_memcpy(&w, &v, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, CPOL_SC1);
+}
+__device__ __forceinline__ void wt_store8(__amdgpu_buffer_rsrc_t r, int off, double v) {
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  u2 w;
+  __builtin_memcpy(&w, &v, 8);
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, off, 0, CPOL_SC1);
+}
+// a value every lane of the wave holds (e.g. the block's first env), as a scalar
+__device__ __forceinline__ int64_t uniform_i64(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
 struct SpecDev {
@@ -124,6 +162,7 @@ struct StepArgs {
   const double* lut64;
   const uint32_t* episode;    // device word written by the reset kernel (graph-replay safe)
   double* metrics;            // [n][4 + N] evaluation-harness accumulators (imenv_set_episode_metrics) or null
+  uint64_t* stamps;           // diagnostics (IMENV_STAMPS builds): [waves][8] s_memrealtime phase stamps, or null
   int64_t n;
   uint32_t env_offset;
   int32_t t;
@@ -296,6 +335,30 @@ __device__ __forceinline__ void load_words(const void* __restrict__ p, uint32_t 
   }
 }
 
+// store_words as write-through buffer stores at byte offset off of resource r
+template <int BYTES>
+__device__ __forceinline__ void wt_store_words(__amdgpu_buffer_rsrc_t r, int off, const uint32_t (&w)[BYTES / 4]) {
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  constexpr int W = BYTES / 4;
+  if constexpr (BYTES % 16 == 0) {
+#pragma unroll
+    for (int q = 0; q < W / 4; ++q) {
+      const u4 x = {w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+      __builtin_amdgcn_raw_buffer_store_b128(x, r, off + 16 * q, 0, CPOL_SC1);
+    }
+  } else if constexpr (BYTES % 8 == 0) {
+#pragma unroll
+    for (int q = 0; q < W / 2; ++q) {
+      const u2 x = {w[2 * q], w[2 * q + 1]};
+      __builtin_amdgcn_raw_buffer_store_b64(x, r, off + 8 * q, 0, CPOL_SC1);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < W; ++q) __builtin_amdgcn_raw_buffer_store_b32(w[q], r, off + 4 * q, 0, CPOL_SC1);
+  }
+}
+
 template <int BYTES>
 __device__ __forceinline__ void store_words(void* __restrict__ p, const uint32_t (&w)[BYTES / 4]) {
   constexpr int W = BYTES / 4;
@@ -383,6 +446,20 @@ struct Row {
 #pragma unroll
       for (int i = 0; i < NT; ++i) if (i < N) base[e * np + i] = (ST)v[i];
     }
+  }
+
+  // write-through form for exact rows: e0 is the wave-uniform first env, lane = e - e0
+  __device__ static __forceinline__ void store_wt(ST* __restrict__ base, int64_t e0, int lane, const int (&v)[NT]) {
+    uint32_t w[WORDS];
+#pragma unroll
+    for (int q = 0; q < WORDS; ++q) w[q] = 0;
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      if constexpr (ES == 1) w[i >> 2] |= ((uint32_t)(uint8_t)v[i]) << ((i & 3) * 8);
+      else if constexpr (ES == 2) w[i >> 1] |= ((uint32_t)(uint16_t)(int16_t)v[i]) << ((i & 1) * 16);
+      else w[i] = (uint32_t)v[i];
+    }
+    wt_store_words<BYTES>(wt_rsrc(base + e0 * NPT), lane * BYTES, w);
   }
 };
 
@@ -1014,13 +1091,28 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
     int net[NT];
 #pragma unroll
     for (int i = 0; i < NT; ++i) net[i] = inv[i] - bl[i];   // inv[i] * bl[i] == 0 after step_core
-    RN::store(p_net, e, np, N, net);
-    R::store(p_ou, e, np, N, ou);
+    if constexpr (IMENV_WT_STATE && EXACT) {
+      const int64_t e0 = uniform_i64(e - tid);
+      RN::store_wt(p_net, e0, tid, net);
+      R::store_wt(p_ou, e0, tid, ou);
 #pragma unroll
-    for (int i = 0; i < NT; ++i)
-      if (i < N) p_ring[(int64_t)A.ring_row[i] * n + e] = (ST)push[i];
-    if (p.noisy_delay()) RC::store(p_carry, e, np, N, cout);
-    if (MC > 0) R32::store(p_bto, e, np, N, btoc);
+      for (int i = 0; i < NT; ++i) {
+        const auto rr = wt_rsrc(p_ring + (int64_t)A.ring_row[i] * n + e0);
+        if constexpr (sizeof(ST) == 1) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)push[i], rr, tid, 0, CPOL_SC1);
+        else if constexpr (sizeof(ST) == 2) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)push[i], rr, 2 * tid, 0, CPOL_SC1);
+        else __builtin_amdgcn_raw_buffer_store_b32((uint32_t)push[i], rr, 4 * tid, 0, CPOL_SC1);
+      }
+      if (p.noisy_delay()) RC::store_wt(p_carry, e0, tid, cout);
+      if (MC > 0) R32::store_wt(p_bto, e0, tid, btoc);
+    } else {
+      RN::store(p_net, e, np, N, net);
+      R::store(p_ou, e, np, N, ou);
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+        if (i < N) p_ring[(int64_t)A.ring_row[i] * n + e] = (ST)push[i];
+      if (p.noisy_delay()) RC::store(p_carry, e, np, N, cout);
+      if (MC > 0) R32::store(p_bto, e, np, N, btoc);
+    }
     if (!split_ok) {          // no-return atomics
       atomicOr(A.err + e, 1u);
       atomicOr(A.err_any, 1u);
@@ -1035,6 +1127,9 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
       for (int i = 0; i < NT; ++i) if (i < N) A.reward[e * N + i] = prof[i];
     } else if constexpr (IMENV_NT_STORE) {
       __builtin_nontemporal_store(rew, A.reward + e);
+    } else if constexpr (IMENV_WT_STORE) {
+      const int64_t e0 = uniform_i64(e - tid);     // the block's first env of this slab
+      wt_store8(wt_rsrc(A.reward + e0), tid * 8, rew);
     } else {
       A.reward[e] = rew;
     }
@@ -1219,14 +1314,25 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   const int64_t n = A.n;
   const int64_t eb = (int64_t)blockIdx.x * EPT * BS;
   const bool poisson = p.demand_layout() == IMENV_LAYOUT_DRAW && p.demand_dist() == IMENV_DEMAND_POISSON;
+  // diagnostic phase stamps (IMENV_STAMPS builds, 10 ns ticks of s_memrealtime): 0 entry, 1 loads issued,
+  // 2 loads landed (an added vmcnt(0) wait), 3 computed, 4 after the slab barrier, 5 stores issued,
+  // 6 stores acknowledged
+  [[maybe_unused]] uint64_t stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if constexpr (IMENV_STAMPS) stamp[0] = __builtin_amdgcn_s_memrealtime();
   StepLoad<P> L[EPT];
 #pragma unroll
   for (int k = 0; k < EPT; ++k) step_load(p, A, eb + k * BS + tid, L[k]);
   p.stage_tables(s_tab, poisson);
   constexpr int SSTR = stage_stride<P>();
   constexpr int SLAB = BS * SSTR * (P::OBS_STAGE64 ? 2 : 1);   // floats per BS-env slab
+  if constexpr (IMENV_STAMPS) {
+    stamp[1] = __builtin_amdgcn_s_memrealtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp[2] = __builtin_amdgcn_s_memrealtime();
+  }
 #pragma unroll
   for (int k = 0; k < EPT; ++k) step_finish(p, A, eb + k * BS + tid, L[k], s_tab, s_obs + k * SLAB);
+  if constexpr (IMENV_STAMPS) stamp[3] = __builtin_amdgcn_s_memrealtime();
   // Write-out group: the block (one barrier), or with IMENV_WAVE_SLAB each wave on its own (the 64 rows
   // it staged itself: LDS ops of one wave complete in order, so a wavefront fence replaces the block
   // barrier and no wave waits for its block's slowest wave)
@@ -1243,6 +1349,7 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
       }
     }
   }
+  if constexpr (IMENV_STAMPS) stamp[4] = __builtin_amdgcn_s_memrealtime();
   if constexpr (SROW > 0 && P::OBS_STAGE64) {
     // float64 rows: the same write-out in 16-byte double2 runs
     if (staged_obs(p)) {
@@ -1259,8 +1366,13 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           // 16-byte stores need a 16-byte aligned destination (a caller's obs_out view may be offset)
           if ((total & 1) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0) {
             double2* g2 = reinterpret_cast<double2*>(gobs);
-            for (int q = gl; q < total / 2; q += GS)
-              store16<IMENV_NT_STORE>(g2 + q, make_double2(at(so, 2 * q), at(so, 2 * q + 1)));
+            if constexpr (IMENV_WT_STORE) {
+              const auto rs = wt_rsrc(gobs);
+              for (int q = gl; q < total / 2; q += GS) wt_store16(rs, q * 16, make_double2(at(so, 2 * q), at(so, 2 * q + 1)));
+            } else {
+              for (int q = gl; q < total / 2; q += GS)
+                store16<IMENV_NT_STORE>(g2 + q, make_double2(at(so, 2 * q), at(so, 2 * q + 1)));
+            }
           } else {
             for (int q = gl; q < total; q += GS) gobs[q] = at(so, q);
           }
@@ -1282,7 +1394,16 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           const float* so = s_obs + k * SLAB + gi * GS * SSTR;
           if ((total & 3) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0) {
             float4* g4 = reinterpret_cast<float4*>(gobs);
-            if constexpr (SSTR == row) {
+            if constexpr (IMENV_WT_STORE) {
+              const auto rs = wt_rsrc(gobs);
+              if constexpr (SSTR == row) {
+                const float4* s4 = reinterpret_cast<const float4*>(so);
+                for (int q = gl; q < total / 4; q += GS) wt_store16(rs, q * 16, s4[q]);
+              } else {
+                for (int q = gl; q < total / 4; q += GS)
+                  wt_store16(rs, q * 16, make_float4(at(so, 4 * q), at(so, 4 * q + 1), at(so, 4 * q + 2), at(so, 4 * q + 3)));
+              }
+            } else if constexpr (SSTR == row) {
               const float4* s4 = reinterpret_cast<const float4*>(so);
               for (int q = gl; q < total / 4; q += GS) store16<IMENV_NT_STORE>(g4 + q, s4[q]);
             } else {
@@ -1295,6 +1416,17 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           }
         }
       }
+    }
+  }
+  if constexpr (IMENV_STAMPS) {
+    stamp[5] = __builtin_amdgcn_s_memrealtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp[6] = __builtin_amdgcn_s_memrealtime();
+    stamp[7] = ((uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) << 32) | blockIdx.x;  // XCC id
+    if (A.stamps && (tid & 63) == 0) {
+      uint64_t* o = A.stamps + ((int64_t)blockIdx.x * (BS / 64) + tid / 64) * 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = stamp[k];
     }
   }
 }

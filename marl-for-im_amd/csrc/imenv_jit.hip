@@ -202,6 +202,8 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
   const int obs_row = jit_obs_row(d, base, bs, f.obs_f64 ? 8 : 4);
   const bool inline_tab = d.table_len <= kInlineTable;
   if (f.stream_store) o << "#define IMENV_NT_STORE 1\n";
+  if (f.wt_obs) o << "#define IMENV_WT_STORE 1\n";
+  if (f.wt_state) o << "#define IMENV_WT_STATE 1\n";
   o << "#include \"imenv_device.h\"\n"
        "// generated by imenv_jit.hip: every spec value is a compile-time constant\n"
        "struct JitSpec {\n";
@@ -303,9 +305,11 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
 }
 }  // namespace
 
-// the streaming-store variant has a name of its own, so kernel traces and PMC summaries never
-// average it with the plain-store kernel
-static const char* jit_kernel_name(const JitFlags& f) { return f.stream_store ? "imenv_step_jit_nt" : "imenv_step_jit"; }
+// the streaming- and write-through-store variants have names of their own, so kernel traces and PMC
+// summaries never average them with the plain-store kernel
+static const char* jit_kernel_name(const JitFlags& f) {
+  return f.stream_store ? "imenv_step_jit_nt" : (f.wt_obs || f.wt_state) ? "imenv_step_jit_wt" : "imenv_step_jit";
+}
 
 std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f) {
   std::ostringstream o;

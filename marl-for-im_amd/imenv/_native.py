@@ -28,7 +28,7 @@ OBS_ZERO, OBS_RAW, OBS_SCALED, OBS_CLAMP_SCALED = 0, 1, 2, 3
 DEMAND_CUSTOM, DEMAND_POISSON, DEMAND_UNIFORM = 1, 2, 3
 LAYOUT_DRAW, LAYOUT_PER_ENV, LAYOUT_BROADCAST = 0, 1, 2
 F32, F64 = 0, 1
-STORE_DEFAULT, STORE_STREAM = 0, 1
+STORE_DEFAULT, STORE_STREAM, STORE_PLAIN, STORE_WRITETHROUGH = 0, 1, 2, 3
 PLAN_SHARED, PLAN_PER_EPISODE = 0, 1
 STAT_RETURN, STAT_OBJECTIVE, STAT_INVENTORY, STAT_BACKLOG, STAT_CUSTOMER_BACKLOG = range(5)
 NUM_STATS = 5
@@ -104,6 +104,7 @@ SYMBOLS = [
     ("imenv_set_delay_uniforms", c_int, [c_void_p, c_int32, c_void_p, c_void_p]),
     ("imenv_set_jit", c_int, [c_void_p, c_int]),
     ("imenv_set_store_policy", c_int, [c_void_p, c_int]),
+    ("imenv_debug_stamps", c_int, [c_void_p, c_void_p, c_int64, POINTER(c_int64)]),
     ("imenv_kernel_info", c_int, [c_void_p, ctypes.c_char_p, c_int64]),
     ("imenv_jit_check", c_int, [POINTER(ImEnvSpec), ctypes.c_char_p, c_uint32, ctypes.c_char_p, c_int64]),
     ("imenv_destroy", None, [c_void_p]),

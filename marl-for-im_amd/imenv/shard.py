@@ -65,6 +65,7 @@ class PackedGather:
                       for _ in range(buffers)]
         self._work = [None] * buffers
         self._into = dist.get_backend(group) == "nccl"
+        self._kept = None       # completed collectives, kept for timing (keep_works)
 
     def _field(self, buf, j, lead=()):
         shape, dtype = self.fields[j]
@@ -97,6 +98,16 @@ class PackedGather:
         if w is not None:
             w.wait()          # NCCL: a stream dependency, not a host block
             self._work[k] = None
+            if self._kept is not None:
+                self._kept.append(w)
+
+    def keep_works(self, on):
+        """Start (on=True) or stop keeping every collective's Work object once it has been waited for
+        (bench.py reads each one's own duration, Work._get_duration, with TORCH_NCCL_ENABLE_TIMING=1).
+        Returns the Works kept so far."""
+        kept = self._kept or []
+        self._kept = [] if on else None
+        return kept
 
     def __call__(self, *tensors, k=0):
         """Copy tensors into send buffer k, gather synchronously, return the [world, ...] views."""

@@ -351,12 +351,19 @@ class VectorInvEnv:
             per.append(b)
         return per
 
+    STORE_POLICIES = ("default", "stream", "plain", "writethrough")
+
     def set_store_policy(self, policy):
-        """"default": plain observation / reward stores (a policy reads them right after the step);
-        "stream": non-temporal stores for outputs bound for a rollout buffer read later (faster
-        step, slower immediate consumer). Same results either way."""
-        code = {"default": nat.STORE_DEFAULT, "stream": nat.STORE_STREAM}[policy]
-        nat.check(self.lib.imenv_set_store_policy(self._h, code), "imenv_set_store_policy")
+        """Store policy of the step kernel's outputs (imenv.h); same results under all:
+        "default": write-through observation / reward stores (nothing left dirty in L2 for the
+        end-of-launch write-back), the state rows too for batches whose outputs fit in L2;
+        "stream": non-temporal stores (outputs read much later, e.g. a rollout buffer);
+        "plain": plain cached stores; "writethrough": write-through for every store."""
+        codes = dict(zip(self.STORE_POLICIES, (nat.STORE_DEFAULT, nat.STORE_STREAM, nat.STORE_PLAIN,
+                                               nat.STORE_WRITETHROUGH)))
+        if policy not in codes:
+            raise ValueError("store policy must be one of %s" % (self.STORE_POLICIES,))
+        nat.check(self.lib.imenv_set_store_policy(self._h, codes[policy]), "imenv_set_store_policy")
 
     def set_jit(self, mode):
         """1: hipRTC kernel specialised for this spec (default); 0: ahead-of-time kernels."""

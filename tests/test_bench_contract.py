@@ -50,13 +50,60 @@ def test_bench_json_line(steps, warmup):
     assert r["kernel"].startswith("jit:imenv_step_jit")
     assert r["kernel_samples"] == steps and r["kernel_us"] > 0
     assert r["store_policy"] == "default"
-    alt = r["alt_store_policy"]      # the other store policy, timed the same way (informational)
-    assert alt["store_policy"] == "stream" and alt["value"] > 0 and 0 < alt["frac"] < 1
-    # the line names the kernel it timed (plain stores), the informational run its own (flag 0x800)
-    assert r["kernel"].startswith("jit:imenv_step_jit[") and ",flags=0x0," in r["kernel"]
-    assert alt["kernel"].startswith("jit:imenv_step_jit_nt[") and ",flags=0x800," in alt["kernel"]
+    alt = r["alt_store_policy"]      # plain stores, timed the same way (informational)
+    assert alt["store_policy"] == "plain" and alt["value"] > 0 and 0 < alt["frac"] < 1
+    # the line names the kernel it timed: write-through obs / reward stores (0x2000), and at 2^20 envs
+    # (58.7 MB of outputs per launch, more than L2) plain state rows; the informational run its own
+    assert r["kernel"].startswith("jit:imenv_step_jit_wt[") and ",flags=0x2000," in r["kernel"]
+    assert alt["kernel"].startswith("jit:imenv_step_jit[") and ",flags=0x0," in alt["kernel"]
+    g = r["graph"]                   # the HIP-graph-replayed episode (informational)
+    assert g["steps"] == 30 * g["replays"] and g["ms_per_step"] > 0 and g["kernel"] == r["kernel"]
+    assert d["resets_timed"] == sum(1 for s in range(warmup, warmup + steps) if s % 30 == 0)
+    assert ("%d of them preceded by the episode's reset kernel" % d["resets_timed"]) in d["config"]["workload"]
+    assert d["ranks_seen"] == 1 and d["launcher"] == "none"
     assert 90 < r["bytes_per_env_step"] <= r["bytes_per_env_step_steady"]
     if steps != 20:
         return
     c = d["cpu_baseline"]
     assert c["value"] > 0 and c["kind"] == "port" and c["cores"] >= 1
+
+
+def _run_rc(args, timeout, **extra_env):
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1", **extra_env)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        if k not in extra_env:
+            env.pop(k, None)
+    return subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, timeout=timeout, env=env,
+                          cwd=ROOT)
+
+
+def test_gpus_n_spawns_n_ranks_itself():
+    """`bench.py --gpus 2` with no launcher starts its own 2 rank processes (gloo rendezvous on
+    127.0.0.1, census of ranks, max-reduction), hands them the CPU baseline it measured first, and
+    rank 0 prints one line with n_gpus 2 and ranks_seen 2 (the reference's own parallelism: one env
+    per RLlib worker process, hyperparams.py:14)."""
+    r = _run_rc(["--gpus", "2", "--dry-run", "--cpu-seconds", "0.2"], timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout           # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["launcher"] == "self"
+    assert sorted(x["rank"] for x in d["ranks"]) == [0, 1] and d["max_over_ranks"] == 2.0
+    assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["kind"] == "port"
+
+
+def test_gpus_disagreeing_with_launcher_world_fails():
+    r = _run_rc(["--gpus", "2", "--dry-run", "--no-cpu-baseline"], timeout=120, WORLD_SIZE="1", RANK="0",
+                LOCAL_RANK="0")
+    assert r.returncode == 2 and "launcher started 1 ranks" in r.stderr
+
+
+def test_a_failing_rank_fails_the_launch():
+    r = _run_rc(["--gpus", "2", "--dry-run", "--no-cpu-baseline"], timeout=120, IMENV_BENCH_DRY_FAIL_RANK="1")
+    assert r.returncode == 7, (r.returncode, r.stderr[-2000:])
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_steps_must_be_positive():
+    r = _run_rc(["--steps", "0", "--no-cpu-baseline"], timeout=60)
+    assert r.returncode == 2 and "--steps must be >= 1" in r.stderr

@@ -117,25 +117,38 @@ def test_gpu_misaligned_obs_out_view(name, odt, mode):
         e.close()
 
 
-@pytest.mark.parametrize("name", ["C2_MAIM4", "C3_IM8", "C4_MAIM_div1", "MAIM_div2_share", "MAIM4_indep"])
+# store policy -> (flag bits that must be set, flag bits that must be clear) in the kernel tag:
+# 0x800 non-temporal obs / reward, 0x2000 write-through obs / reward, 0x4000 write-through state rows
+STORE_FLAGS = {"stream": (0x800, 0x6000), "plain": (0, 0x6800), "writethrough": (0x6000, 0x800),
+               "default": (0x6000, 0x800)}     # default at golden sizes (32 envs: outputs fit in L2)
+
+
+@pytest.mark.parametrize("name", ["C2_MAIM4", "C3_IM8", "C4_MAIM_div1", "MAIM_div2_share", "MAIM4_indep",
+                                  "IM4_td_pd_pa_L2", "MAIM_div1_noisy_delay"])
 @pytest.mark.parametrize("odt", ["f32", "f64"])
-def test_gpu_stream_store_policy_same_results(name, odt):
-    """IMENV_STORE_STREAM (non-temporal observation / reward stores) is a separate hipRTC kernel
-    (flag bit 0x800 in its tag) with bit-identical results; set back to the default, the plain
-    kernel runs again."""
+@pytest.mark.parametrize("policy", ["stream", "plain", "writethrough", "default"])
+def test_gpu_store_policies_same_results(name, odt, policy):
+    """Every store policy (imenv_set_store_policy) is a hipRTC kernel of its own (flag bits in its tag)
+    with bit-identical results against the reference's golden episode; switching policy mid-run
+    selects the other kernel."""
     from imenv import VectorInvEnv
     meta, d = load_case(name)
     tdt = torch.float64 if odt == "f64" else torch.float32
     env = VectorInvEnv(meta["kind"], meta["config"], n_envs=meta["E"], device=DEV, obs_dtype=tdt)
-    env.set_store_policy("stream")
+    env.set_store_policy(policy)
     _episode(env, meta, d, tdt)
     flags = int(re.search(r"flags=0x([0-9a-f]+)", env.kernel_info()).group(1), 16)
-    assert env.kernel_info().startswith("jit:") and flags & 0x800, env.kernel_info()
-    env.set_store_policy("default")
+    on, off = STORE_FLAGS[policy]
+    assert env.kernel_info().startswith("jit:") and flags & on == on and not flags & off, env.kernel_info()
+    other = "plain" if policy != "plain" else "writethrough"
+    env.set_store_policy(other)
     _episode(env, meta, d, tdt)
     flags = int(re.search(r"flags=0x([0-9a-f]+)", env.kernel_info()).group(1), 16)
-    assert not flags & 0x800
+    on, off = STORE_FLAGS[other]
+    assert flags & on == on and not flags & off, env.kernel_info()
     assert env.lib.imenv_set_store_policy(env._h, 7) != 0      # unknown policy: IMENV_E_INVALID
+    with pytest.raises(ValueError):
+        env.set_store_policy("bogus")
     env.close()
 
 

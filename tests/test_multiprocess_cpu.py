@@ -124,6 +124,7 @@ def _packed_worker(rank, world, port, out_path):
         n, N, F, T = 5, 4, 3, 30
         # per-step, double-buffered: write step t into buffer t % 2 while step t-1's gather is in flight
         g = StepGather(torch.zeros((n, N, F)), torch.zeros(n, dtype=torch.float64))
+        g.keep_works(True)       # bench.py --gather times each collective from its kept Work
         steps = []
         for t in range(6):
             g.obs_out(t).copy_(torch.full((n, N, F), 100.0 * rank + t))
@@ -132,6 +133,9 @@ def _packed_worker(rank, world, port, out_path):
             if t >= 1:
                 steps.append([x.clone() for x in g.result(t - 1)])
         steps.append([x.clone() for x in g.result(5)])
+        kept = g.keep_works(False)
+        assert len(kept) == 6 and all(w.is_completed() for w in kept), len(kept)
+        assert g.keep_works(False) == []
         # per-episode: one collective over the whole rollout, independent (per-agent) rewards
         eg = EpisodeGather(_EnvShape(T, n, N, F, independent=True))
         eg.obs.copy_(torch.arange((T + 1) * n * N * F, dtype=torch.float32).view(T + 1, n, N, F) + rank)

@@ -112,3 +112,18 @@ def test_jit_plan_rollout_kernel_compiles():
     # a plan rollout with an objective is not a kernel
     spec = build_spec(meta["SHLP4"]["kind"], meta["SHLP4"]["config"]).to_c()
     assert lib.imenv_jit_check(ctypes.byref(spec), b"gfx950", (1 << 12) | ((8 | (2 << 4)) << 13), log, len(log)) != 0
+
+
+def test_library_embeds_the_current_device_sources():
+    """The hipRTC specialiser compiles the step kernel from device sources embedded in libimenv.so at
+    build time (imenv_rtc_src.inc, generated by __graft_entry__.build(), not tracked). A stale library
+    would ship a different kernel body than the one the tests and the oracle were checked against, so
+    the embedded text must equal imenv_device.h and imenv.h byte for byte."""
+    from imenv import _native
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libimenv.so not built")
+    blob = open(_native.LIB_PATH, "rb").read()
+    for path in (os.path.join(ROOT, "marl-for-im_amd", "csrc", "imenv_device.h"), HEADER):
+        text = open(path, "rb").read()
+        assert blob.find(text + b"\0") >= 0, \
+            "%s differs from the copy embedded in libimenv.so: rebuild (python __graft_entry__.py build)" % path

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--n-envs", type=int, default=1 << 20)
     ap.add_argument("--iters", type=int, default=60)
     ap.add_argument("--config", default="C2", help="bench.py config name (C2, C3, C4)")
-    ap.add_argument("--store", default="default", choices=["default", "stream"])
+    ap.add_argument("--store", default="default", choices=["default", "stream", "plain", "writethrough"])
     args = ap.parse_args()
     import torch
     from bench import CONFIGS
