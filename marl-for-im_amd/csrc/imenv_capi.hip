@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -365,6 +366,24 @@ int fail(int code, const std::string& msg) {
     if (_e != hipSuccess) return fail(IMENV_E_HIP, std::string(#x ": ") + hipGetErrorString(_e));    \
   } while (0)
 
+// Integer tuning switch from the environment, read once per process per name (a cached policy, not a
+// getenv per call). Unset or unparsable: dflt.
+int env_switch(const char* name, int dflt) {
+  static std::mutex mu;
+  static std::unordered_map<std::string, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(name);
+  if (it != cache.end()) return it->second;
+  int v = dflt;
+  if (const char* e = std::getenv(name)) {
+    char* end = nullptr;
+    const long x = std::strtol(e, &end, 10);
+    if (end && end != e) v = (int)x;
+  }
+  cache.emplace(name, v);
+  return v;
+}
+
 uint64_t prob_thr32(double p) {
   if (!(p > 0.0)) return 0;   // also NaN: the reference's `uniform() < nan` is never true
   double v = std::ceil(p * 4294967296.0);
@@ -602,6 +621,7 @@ int validate_and_derive(const ImEnvSpec& s, SpecDev& d, int& maxc) {
   }
   // narrowest element type the bounds allow; IMENV_STATE_BYTES=2|4 forces a wider one (testing)
   const int64_t bound = state_bound(s);
+  d.vbound = (int32_t)std::min<int64_t>(std::max<int64_t>(bound, N), INT32_MAX);
   d.es = bound <= 255 ? 1 : (bound <= 32767 ? 2 : 4);
   if (d.es == 1 && net_bound(s) > 127) d.es = 2;   // the net row is signed (int8 beside uint8 rows)
   if (d.es == 1 && (int64_t)s.num_periods * bound > 32767) d.es = 2;   // int16 noisy-delay carry (CarryOf)
@@ -996,6 +1016,10 @@ int imenv_plan_rollout(ImEnv* h, const ImEnvPlanRollout* r, void* stream) {
   if (s.reward_mode == IMENV_REWARD_INDEPENDENT)
     return fail(IMENV_E_UNSUPPORTED, "plan rollout needs a scalar reward (independent multi-agent rewards)");
   if (r->num_plans < 1 || r->num_scenarios < 1) return fail(IMENV_E_INVALID, "num_plans / num_scenarios < 1");
+  // the inventory / backlog sums are sums of the raw state, which equal the LP scripts' sum(s[:, 0]) /
+  // sum(s[:, 1]) only for raw observations (every LP script sets standardise_state False)
+  if (s.group_mode[IMENV_G_INV] != IMENV_OBS_RAW || s.group_mode[IMENV_G_BACKLOG] != IMENV_OBS_RAW)
+    return fail(IMENV_E_UNSUPPORTED, "plan rollout sums raw state: needs standardise_state False (raw observations)");
   if (r->action_dtype != IMENV_F32 && r->action_dtype != IMENV_F64)
     return fail(IMENV_E_INVALID, "action_dtype must be IMENV_F32 or IMENV_F64");
   if (r->plan_layout != IMENV_PLAN_SHARED && r->plan_layout != IMENV_PLAN_PER_EPISODE)
@@ -1126,8 +1150,7 @@ int imenv_cc_observation(int64_t n, int32_t num_agents, int32_t num_features, co
   hipStream_t st = static_cast<hipStream_t>(stream);
   {
     // staged (env, agent)-row kernel when the block's slab fits 48 KiB
-    int BSC = 256;                                    // IMENV_CC_BS=512: 512-thread blocks (tuning)
-    if (const char* v = std::getenv("IMENV_CC_BS")) BSC = std::atoi(v) == 512 ? 512 : 256;
+    const int BSC = env_switch("IMENV_CC_BS", 256) == 512 ? 512 : 256;   // 512-thread blocks (tuning)
     const int N = num_agents, F = num_features, W = N * F + N - 1, E = BSC / N;
     const size_t osz = obs_dtype == IMENV_F64 ? 8 : 4;
     const size_t lds = (size_t)E * N * 8 + (size_t)E * N * F * osz + (size_t)E * N * (W | 1) * osz;
@@ -1136,8 +1159,10 @@ int imenv_cc_observation(int64_t n, int32_t num_agents, int32_t num_features, co
       // non-temporal row stores (default; IMENV_CC_NT=0 turns them off): the rows are read back only by
       // a later training pass, and streamed past the caches the kernel runs at 76% of HBM peak instead
       // of 54% (tools/bench_kernels.py, 2^20 envs, profiles/r02/kernels_cc_nt.log)
-      const bool nt = !(std::getenv("IMENV_CC_NT") && std::atoi(std::getenv("IMENV_CC_NT")) == 0);
-      if (BSC == 512)
+      const bool nt = env_switch("IMENV_CC_NT", 1) != 0;
+      if (BSC == 512 && nt)
+        launch_cc_slab<512, true>(g, lds, st, obs, obs_dtype, actions, action_dtype, n, N, F, clip_lo, clip_hi, out);
+      else if (BSC == 512)
         launch_cc_slab<512, false>(g, lds, st, obs, obs_dtype, actions, action_dtype, n, N, F, clip_lo, clip_hi, out);
       else if (nt)
         launch_cc_slab<256, true>(g, lds, st, obs, obs_dtype, actions, action_dtype, n, N, F, clip_lo, clip_hi, out);
@@ -1184,7 +1209,7 @@ int imenv_gae(int64_t n, int32_t T, const void* rewards, int reward_dtype, const
   // non-temporal advantage / value-target stores (default; IMENV_GAE_NT=0 turns them off): they are
   // read by the loss pass after the whole batch, and streamed the kernel takes 109 us instead of
   // 113-116 us for 2^20 envs x 30 periods (profiles/r02/kernels_gae_nt.log)
-  const bool nt = !(std::getenv("IMENV_GAE_NT") && std::atoi(std::getenv("IMENV_GAE_NT")) == 0);
+  const bool nt = env_switch("IMENV_GAE_NT", 1) != 0;
   auto launch = [&](auto nt_tag) {
     constexpr bool NTS = decltype(nt_tag)::value;
     if (reward_dtype == IMENV_F32 && value_dtype == IMENV_F32)

@@ -123,6 +123,7 @@ struct SpecDev {
   int32_t ring_total;                       // ring rows = sum of delays
   int32_t np;                               // packed row length (elements)
   int32_t es;                               // state element bytes: 1 (uint8), 2 (int16) or 4 (int32)
+  int32_t vbound;                           // proven bound of every raw value an observation reads (>= N)
   int32_t table_len;
   uint32_t table[IMENV_TABLE_MAX];          // Poisson inversion thresholds
   uint16_t guide[1 << IMENV_GUIDE_BITS];    // indexed-search guide: #{thresholds <= g << (32 - bits)}
@@ -793,13 +794,30 @@ template <class P>
 constexpr int stage_row() {
   return (P::BASE && P::NT <= 8) ? 3 * P::NT : (!P::BASE ? P::OBS_ROW : 0);
 }
-// Values between consecutive envs of the slab. Each lane writes its own row, so a row of a multiple of
-// 8 floats (or an even number of doubles) puts a wave's writes into bank conflicts (64 floats: every
-// lane in one bank); such rows get one pad value and the write-out gathers them back into packed order.
+// Values between consecutive envs of the slab. Each lane writes its own row. float32 rows of a multiple
+// of 4 values are written and read as float4 (ds_write_b128 / ds_read_b128: 16 B per lane, no index
+// arithmetic in the write-out); a multiple of 8 puts a wave's 16-byte writes on a bank period of 8
+// dwords, so such rows get 4 pad values (stride = row + 4, which keeps the 16-byte alignment and
+// spreads 8 consecutive lanes over all 32 banks). Other rows, and float64 rows of an even length
+// (one pad value), are written value by value and gathered back into packed order.
 template <class P>
 constexpr int stage_stride() {
-  return (stage_row<P>() > 0 && stage_row<P>() % (P::OBS_STAGE64 ? 2 : 8) == 0) ? stage_row<P>() + 1
-                                                                                 : stage_row<P>();
+  constexpr int r = stage_row<P>();
+  if (r <= 0) return r;
+  if (P::OBS_STAGE64) return r % 2 == 0 ? r + 1 : r;
+  return r % 8 == 0 ? r + 4 : r;
+}
+// One lane's float32 row into its LDS slot (16-byte stores when the row and the stride allow them).
+template <int ROW, int SSTR>
+__device__ __forceinline__ void lds_row_store(float* __restrict__ s, const float (&v)[ROW]) {
+  if constexpr (ROW % 4 == 0 && SSTR % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < ROW / 4; ++q)
+      reinterpret_cast<float4*>(s)[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < ROW; ++k) s[k] = v[k];
+  }
 }
 // Whether this call's observations go through the slab (the slab's value type matches the call's).
 template <class P>
@@ -1186,6 +1204,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   if constexpr (P::BASE) {
     if (STAGE && staged_obs(p)) {
       constexpr int row = stage_stride<P>();
+      [[maybe_unused]] float rv32[3 * NT];   // the env's float32 row, stored to LDS in one go
       if (valid) {
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
@@ -1196,12 +1215,13 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
               sd[tid * row + 3 * i + 1] = p.obs64(IMENV_G_BACKLOG, i, bl[i], A.lut64);
               sd[tid * row + 3 * i + 2] = p.obs64(IMENV_G_ORDER_U, i, ou[i], A.lut64);
             } else {
-              s_obs[tid * row + 3 * i + 0] = p.obs32(IMENV_G_INV, i, inv[i], A.lut32);
-              s_obs[tid * row + 3 * i + 1] = p.obs32(IMENV_G_BACKLOG, i, bl[i], A.lut32);
-              s_obs[tid * row + 3 * i + 2] = p.obs32(IMENV_G_ORDER_U, i, ou[i], A.lut32);
+              rv32[3 * i + 0] = p.obs32(IMENV_G_INV, i, inv[i], A.lut32);
+              rv32[3 * i + 1] = p.obs32(IMENV_G_BACKLOG, i, bl[i], A.lut32);
+              rv32[3 * i + 2] = p.obs32(IMENV_G_ORDER_U, i, ou[i], A.lut32);
             }
           }
         }
+        if constexpr (!P::OBS_STAGE64) lds_row_store<3 * NT, row>(s_obs + tid * row, rv32);
       }
     } else if (valid) {
 #pragma unroll
@@ -1226,6 +1246,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
     const int F = p.num_features();
     const int L = p.prev_length();
     const int tp = t + 1;   // observation period
+    [[maybe_unused]] float rv32[OROW > 0 ? OROW : 1];   // staged float32 row (JIT: constant indices)
     auto feature = [&](const int f) {
       const int g = p.feat_group(f);
       const int j = p.feat_index(f);
@@ -1284,7 +1305,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
             else
               static_cast<double*>(A.obs)[idx] = p.obs64(g, i, v[i], A.lut64);
           } else if constexpr (OROW > 0 && !P::OBS_STAGE64) {
-            s_obs[tid * stage_stride<P>() + i * F + f] = p.obs32(g, i, v[i], A.lut32);
+            rv32[i * F + f] = p.obs32(g, i, v[i], A.lut32);
           } else {
             static_cast<float*>(A.obs)[idx] = p.obs32(g, i, v[i], A.lut32);
           }
@@ -1297,6 +1318,9 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
     } else {
 #pragma unroll 1
       for (int f = 0; f < F; ++f) feature(f);
+    }
+    if constexpr (OROW > 0 && !P::OBS_STAGE64) {
+      if (!p.obs_f64()) lds_row_store<OROW, stage_stride<P>()>(s_obs + tid * stage_stride<P>(), rv32);
     }
   }
 }
@@ -1399,6 +1423,9 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
               if constexpr (SSTR == row) {
                 const float4* s4 = reinterpret_cast<const float4*>(so);
                 for (int q = gl; q < total / 4; q += GS) wt_store16(rs, q * 16, s4[q]);
+              } else if constexpr (row % 4 == 0 && SSTR % 4 == 0) {
+                for (int q = gl; q < total / 4; q += GS)
+                  wt_store16(rs, q * 16, *reinterpret_cast<const float4*>(so + (q / (row / 4)) * SSTR + (q % (row / 4)) * 4));
               } else {
                 for (int q = gl; q < total / 4; q += GS)
                   wt_store16(rs, q * 16, make_float4(at(so, 4 * q), at(so, 4 * q + 1), at(so, 4 * q + 2), at(so, 4 * q + 3)));
@@ -1406,6 +1433,10 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
             } else if constexpr (SSTR == row) {
               const float4* s4 = reinterpret_cast<const float4*>(so);
               for (int q = gl; q < total / 4; q += GS) store16<IMENV_NT_STORE>(g4 + q, s4[q]);
+            } else if constexpr (row % 4 == 0 && SSTR % 4 == 0) {
+              for (int q = gl; q < total / 4; q += GS)
+                store16<IMENV_NT_STORE>(g4 + q, *reinterpret_cast<const float4*>(so + (q / (row / 4)) * SSTR +
+                                                                                  (q % (row / 4)) * 4));
             } else {
               for (int q = gl; q < total / 4; q += GS)
                 store16<IMENV_NT_STORE>(g4 + q, make_float4(at(so, 4 * q), at(so, 4 * q + 1), at(so, 4 * q + 2),

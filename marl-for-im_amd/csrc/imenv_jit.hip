@@ -6,6 +6,7 @@
 // build time (imenv_rtc_src.inc, written by __graft_entry__.build()).
 #include <hip/hiprtc.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -82,7 +83,11 @@ int general_row(const SpecDev& d, bool base) { return base ? 0 : d.s.num_nodes *
 int staged_row(const SpecDev& d, bool base) {
   return base ? (d.s.num_nodes <= 8 ? 3 * d.s.num_nodes : 0) : general_row(d, base);
 }
-int staged_stride(int row, int vbytes) { return (row > 0 && row % (vbytes == 8 ? 2 : 8) == 0) ? row + 1 : row; }
+int staged_stride(int row, int vbytes) {   // = imenv_device.h stage_stride
+  if (row <= 0) return row;
+  if (vbytes == 8) return row % 2 == 0 ? row + 1 : row;
+  return row % 8 == 0 ? row + 4 : row;
+}
 int64_t slab_bytes(const SpecDev& d, bool base, int bs, int vbytes, int ept) {
   return (int64_t)bs * ept * staged_stride(staged_row(d, base), vbytes) * vbytes;
 }
@@ -124,11 +129,16 @@ std::string flit(float x) {
   return buf;
 }
 
-// Observation hooks. The tabulated range [0, lut_max] of every scaled (group, node) is small, so the
-// generator tries cheap closed forms and keeps one only if it reproduces the reference expression
-// bit for bit at EVERY value of that range (exhaustive check here, on the host); anything else,
-// and values outside the range, go through the lookup table / full expression. With one FMA per
-// value the kernel avoids a dependent round trip of table gathers after its arithmetic.
+// Observation hooks. The generator tries cheap closed forms for every scaled (group, node) and keeps
+// one only if it reproduces the reference expression bit for bit at EVERY raw value the observation
+// can see (exhaustive check here, on the host). That range is [0, vbound], the bound validate_and_derive
+// proves for every state value (capacities, capped or T-period backlog, demand, shipments + split
+// overshoot, node ids); a clamped group (MAIM_div's in-transit slots) is clamped first. When the whole
+// proven range is verified (up to kVerifyMax values) the form is emitted without a range guard, so
+// the kernel spends no compare-and-branch per value; otherwise it is guarded by the tabulated range and
+// values outside it take the reference expression (an IEEE double division: exact for every value).
+constexpr int64_t kVerifyMax = 1 << 16;
+
 void emit_obs_hooks(std::ostream& o, const SpecDev& d) {
   const ImEnvSpec& s = d.s;
   const bool use = !(std::getenv("IMENV_JIT_OBS") && std::string(std::getenv("IMENV_JIT_OBS")) == "lut");
@@ -141,9 +151,20 @@ void emit_obs_hooks(std::ostream& o, const SpecDev& d) {
       if (mx < 0) continue;
       const double d1 = (s.b - s.a) / s.group_den[g][i];
       const float c1 = (float)d1, c0 = (float)s.a;
+      // the range to verify: the proven bound, or the clamp when that is smaller and integral
+      const double clip = s.group_clip[g][i];
+      const bool clamp = mode == IMENV_OBS_CLAMP_SCALED;
+      const bool int_clip = clamp && clip >= 0.0 && clip == std::floor(clip) && clip < (double)kVerifyMax;
+      int64_t hi = d.vbound;
+      bool full = hi <= kVerifyMax;
+      if (clamp) {
+        if (int_clip) { hi = std::min<int64_t>(hi, (int64_t)clip); full = true; }
+        else full = false;
+      }
+      if (!full) hi = mx;
       bool k1 = true, k2 = true, k3 = true, q1 = true, q2 = true;
-      for (int v = 0; v <= mx; ++v) {
-        const double e = ref_obs(s, g, i, v);
+      for (int64_t v = 0; v <= hi; ++v) {
+        const double e = ref_obs(s, g, i, (int)v);
         const float e32 = (float)e;
         const float r1 = std::fmaf((float)v, c1, c0);
         const float r2 = (float)std::fma((double)v, d1, s.a);
@@ -156,19 +177,24 @@ void emit_obs_hooks(std::ostream& o, const SpecDev& d) {
         q1 = q1 && std::memcmp(&s1, &e, 8) == 0;
         q2 = q2 && std::memcmp(&s2, &e, 8) == 0;
       }
-      const std::string guard = "if ((unsigned)v <= " + std::to_string(mx) + "u) return ";
+      // guard (partial verification) or clamp (clamped group verified up to its integral clip)
+      std::string pre;
+      if (!full) pre = "if ((unsigned)v <= " + std::to_string(mx) + "u) ";
+      else if (int_clip) pre = "v = v < " + std::to_string((long long)clip) + " ? v : " + std::to_string((long long)clip) + "; ";
+      const std::string ret = full ? "return " : "return ";
+      const std::string tail = full ? ";\n" : "; break;\n";
       const std::string cs = "    case " + std::to_string(g * 256 + i) + ": ";
       // no verified closed form: the reference expression itself (IEEE double division: exact for every
       // v), not a table gather (a dependent gather per value made float64 observations 4-10x slower)
       const std::string direct = "imenv::obs_map(" + std::to_string(mode) + ", (double)v, " + dlit(s.a) + ", " +
                                  dlit(s.b - s.a) + ", " + dlit(s.group_den[g][i]) + ", " +
                                  dlit(s.group_clip[g][i]) + ")";
-      if (k1) c32 << cs << guard << "__builtin_fmaf((float)v, " << flit(c1) << ", " << flit(c0) << "); break;\n";
-      else if (k2) c32 << cs << guard << "(float)__builtin_fma((double)v, " << dlit(d1) << ", " << dlit(s.a) << "); break;\n";
-      else if (k3) c32 << cs << guard << "(float)((double)v * " << dlit(d1) << " + " << dlit(s.a) << "); break;\n";
+      if (k1) c32 << cs << pre << ret << "__builtin_fmaf((float)v, " << flit(c1) << ", " << flit(c0) << ")" << tail;
+      else if (k2) c32 << cs << pre << ret << "(float)__builtin_fma((double)v, " << dlit(d1) << ", " << dlit(s.a) << ")" << tail;
+      else if (k3) c32 << cs << pre << ret << "(float)((double)v * " << dlit(d1) << " + " << dlit(s.a) << ")" << tail;
       else c32 << cs << "return (float)" << direct << ";\n";
-      if (q1) c64 << cs << guard << "__builtin_fma((double)v, " << dlit(d1) << ", " << dlit(s.a) << "); break;\n";
-      else if (q2) c64 << cs << guard << "(double)v * " << dlit(d1) << " + " << dlit(s.a) << "; break;\n";
+      if (q1) c64 << cs << pre << ret << "__builtin_fma((double)v, " << dlit(d1) << ", " << dlit(s.a) << ")" << tail;
+      else if (q2) c64 << cs << pre << ret << "(double)v * " << dlit(d1) << " + " << dlit(s.a) << tail;
       else c64 << cs << "return " << direct << ";\n";
     }
   }
@@ -285,9 +311,21 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
   emit2(o, "int", "lut_off", IMENV_NUM_GROUPS, N, [&](int g, int i) { return ilit(d.lut_off[g][i]); }, "0");
   emit_obs_hooks(o, d);
   if (inline_tab) {
-    // count of thresholds <= w == searchsorted(table, w, 'right') for the sorted table
+    // count of thresholds <= w == searchsorted(table, w, 'right') for the sorted table. The thresholds
+    // are sorted, so once w < thr[K] every later term is 0: the first K thresholds are always counted,
+    // the rest only when some lane of the wave has w >= thr[K] (a wave-uniform branch). K is the first
+    // index whose tail probability 1 - thr[K] / 2^32 is <= 2^-10 (Poisson(5): K = 13 of 24), so a
+    // 64-lane wave takes the tail about 6% of the time and skips ~45% of the compares otherwise.
+    int K = d.table_len;
+    for (int k = 0; k < d.table_len; ++k)
+      if (4294967296.0 - (double)d.table[k] <= 4294967296.0 / 1024.0) { K = k; break; }
     o << "  __device__ static int poisson_draw(uint32_t w, const uint32_t*) {\n    int k = 0;\n";
-    for (int k = 0; k < d.table_len; ++k) o << "    k += (w >= " << d.table[k] << "u) ? 1 : 0;\n";
+    for (int k = 0; k < std::min(K, d.table_len); ++k) o << "    k += (w >= " << d.table[k] << "u) ? 1 : 0;\n";
+    if (K < d.table_len) {
+      o << "    if (__builtin_amdgcn_ballot_w64(w >= " << d.table[K] << "u) != 0) {\n";
+      for (int k = K; k < d.table_len; ++k) o << "      k += (w >= " << d.table[k] << "u) ? 1 : 0;\n";
+      o << "    }\n";
+    }
     o << "    return k;\n  }\n"
          "  __device__ static void stage_tables(uint32_t*, bool) {}\n";
   } else {

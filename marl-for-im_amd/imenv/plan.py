@@ -124,7 +124,8 @@ def replay_plans(env_or_spec, plans, demand, per_episode=True, config=None, devi
     Returns the scripts' lists (lp_reward_list, inventory_list, backlog_list, customer_backlog_list)
     as NumPy arrays and profit [S, T]."""
     spec = getattr(env_or_spec, "spec", env_or_spec)
-    dev = device if device is not None else getattr(getattr(env_or_spec, "_env", None), "device", None)
+    # a drop-in adaptor holds its VectorInvEnv in ._env; a VectorInvEnv has .device itself
+    dev = device if device is not None else getattr(getattr(env_or_spec, "_env", env_or_spec), "device", None)
     pr = PlanRollout(spec, config, device=dev)
     try:
         out = pr.run(plans, demand=demand, per_episode=per_episode)

@@ -48,17 +48,23 @@ class RolloutBuffer:
         adv, vt = buf.advantages()
 
     buf.step(t) launches period t through the env's rollout_stepper (buffers checked once, one C call).
+    obs / actions / rewards are fixed for the buffer's life (the stepper holds their pointers): write
+    into them (buf.actions[t] = a), never rebind them (read-only properties).
     """
 
     def __init__(self, env, obs_dtype=torch.float32):
         # rewards are float64, the dtype the env writes (the reference's profit arithmetic)
         T, n, N, F = env.T, env.n, env.N, env.F
         dev = env.device
-        self.obs = torch.empty((T + 1, n, N, F), dtype=obs_dtype, device=dev)
-        self.actions = torch.empty((T, n, N), dtype=torch.float32, device=dev)
-        self.rewards = torch.empty((T,) + tuple(env.reward_shape()), dtype=torch.float64, device=dev)
+        self._obs = torch.empty((T + 1, n, N, F), dtype=obs_dtype, device=dev)
+        self._actions = torch.empty((T, n, N), dtype=torch.float32, device=dev)
+        self._rewards = torch.empty((T,) + tuple(env.reward_shape()), dtype=torch.float64, device=dev)
         self.values = torch.empty((T, n), dtype=torch.float32, device=dev)
-        self._stepper = env.rollout_stepper(self.actions, self.obs, self.rewards)
+        self._stepper = env.rollout_stepper(self._actions, self._obs, self._rewards)
+
+    obs = property(lambda self: self._obs, doc="[T + 1, n, N, F] observations (row 0: reset)")
+    actions = property(lambda self: self._actions, doc="[T, n, N] float32 actions")
+    rewards = property(lambda self: self._rewards, doc="[T] + reward_shape float64 rewards")
 
     def step(self, t):
         """Step period t of the bound env from actions[t] into obs[t + 1] and rewards[t]; returns done."""

@@ -165,7 +165,9 @@ class VectorInvEnv:
         step of period t with precomputed pointers on the current stream: one C call and no tensor
         checks, for batches small enough that step()'s per-call host work (~9 us) would exceed the
         kernel. t must be the handle's current period (0 after reset()). Returns done (period >= T)
-        like step(). Same kernels, same results as step()."""
+        like step(). Same kernels, same results as step(). The stepper writes into the tensors given
+        here for its whole life (their pointers are taken now): rebinding a buffer means a new
+        stepper. Stepping past the horizon raises like step() does (IMENV_E_DONE)."""
         T, n, N, F = self.T, self.n, self.N, self.F
         ok = (torch.is_tensor(actions) and actions.device == self.device and actions.dtype in _FLOATS
               and actions.is_contiguous() and tuple(actions.shape) == (T, n, N))
@@ -187,6 +189,8 @@ class VectorInvEnv:
         keep = (actions, obs_out, reward_out)
 
         def stepper(t):
+            if t >= T:
+                raise ValueError("stepper(%d): past the horizon of %d periods (reset first)" % (t, T))
             if t != self.period:
                 raise ValueError("stepper(%d) at period %d: the kernel steps the handle's own period" % (t, self.period))
             rc = lib(h, a_ptr[t], adt, o_ptr[t], odt, r_ptr[t], None, done_ref, stream())

@@ -89,5 +89,7 @@ def test_rollout_buffer_with_env():
     for t in range(env2.T):
         assert buf2.step(t) == (t == env2.T - 1)
     assert torch.equal(buf2.obs, buf.obs) and torch.equal(buf2.rewards, buf.rewards)
+    with pytest.raises(AttributeError):       # the stepper holds these tensors: no rebinding
+        buf2.actions = torch.zeros_like(buf2.actions)
     env.close()
     env2.close()

@@ -18,7 +18,9 @@ STAGE_LDS = 48 * 1024      # kStageLds, imenv_jit.hip
 def _episode(env, meta, d, obs_dtype):
     serial = meta["kind"] in ("IM", "MAIM")
     dem = d["customer_demand"]
-    env.reset(customer_demand=dem[:, 0, :] if serial else dem)
+    noisy = meta["noisy"]      # host-fed noisy-delay uniforms, as the reference's session drew them
+    env.reset(customer_demand=dem[:, 0, :] if serial else dem, noisy_delay=bool(noisy), noisy_delay_threshold=noisy,
+              delay_uniforms=d["delay_uniforms"] if noisy else None)
     obs, rew = [], []
     for t in range(meta["T"]):
         a = torch.as_tensor(d["actions"][:, t, :], dtype=torch.float64, device=DEV)
@@ -180,6 +182,8 @@ def test_gpu_rollout_stepper_matches_step(name, odt, rows):
     for t in range(T):
         done = stepper(t)
         assert done == (t == T - 1)
+    with pytest.raises(ValueError, match="past the horizon"):
+        stepper(T)
     got = obs[1:] if rows == "T+1" else obs
     exp = d["obs"] if tdt == torch.float64 else d["obs"].astype(np.float32)
     np.testing.assert_array_equal(got.permute(1, 0, 2, 3).cpu().numpy(), exp)

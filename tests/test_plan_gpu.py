@@ -145,7 +145,16 @@ def test_plan_replay_errors():
     with pytest.raises(ImEnvNativeError, match="scalar reward"):
         pr.run(np.ones((30, 4)), n_scenarios=4)
     pr.close()
-    pr = _pr("IM", gen_cfg.serial4())
+    # raw-state sums only: a standardised-state spec (the LP scripts never use one) is refused
+    pr = _pr("IM", gen_cfg.serial4(standardise_state=True))
+    with pytest.raises(ImEnvNativeError, match="standardise_state"):
+        pr.run(np.ones((30, 4)), n_scenarios=4)
+    pr.close()
+    pr = _pr("MAIM_div", gen_cfg.div1(independent=False))
+    with pytest.raises(ImEnvNativeError, match="standardise_state"):
+        pr.run(np.ones((30, 4)), n_scenarios=4)
+    pr.close()
+    pr = _pr("IM", gen_cfg.serial4(standardise_state=False))
     with pytest.raises(ValueError):
         pr.run(np.ones((30, 3)), n_scenarios=4)                     # wrong node count
     with pytest.raises(ValueError):
@@ -182,9 +191,13 @@ def drawn_plan_case(seed, i):
     tools/fuzz_plan_campaign.py."""
     from fuzz_configs import maybe_order_max, rand_config
     rs = np.random.RandomState(seed)
-    kind = ("IM", "IM_div", "MAIM", "MAIM_div")[i % 4]
+    # the LP scripts replay through raw-state envs (standardise_state False, SHLP_8.py:737-766); a plan
+    # rollout sums the raw state, so standardised-state specs (and MAIM_div, whose observations are
+    # always scaled) are refused (test_plan_replay_errors)
+    kind = ("IM", "IM_div", "MAIM", "IM_div")[i % 4]
     cfg = maybe_order_max(rs, kind, rand_config(rs, kind, (i + i // 4) % 4))   # capacities 5-450
-    if kind in ("MAIM", "MAIM_div"):
+    cfg["standardise_state"] = False
+    if kind == "MAIM":
         cfg["independent"] = False           # the rollout needs a scalar reward
     top = float(np.max(cfg["inv_max"]))
     if i % 3 == 2:
