@@ -382,7 +382,7 @@ int imenv_set_jit(ImEnv* env, int mode);
  *  IMENV_STORE_DEFAULT: observation and reward stores write-through (cache policy sc1: written to
  *    memory at once, nothing left dirty in L2 for the end-of-launch write-back, which otherwise
  *    costs ~bytes / 6 TB/s at every dependent launch boundary); the state rows too when a launch's
- *    observation + reward bytes fit the 32 MiB of L2 (small batches), else plain.
+ *    observation + reward bytes are at most 24 MiB (small batches: L2 is 32 MiB), else plain.
  *  IMENV_STORE_STREAM: non-temporal observation / reward stores (outputs bound for a rollout buffer
  *    read much later).
  *  IMENV_STORE_PLAIN: plain cached stores everywhere (the round-2 default).

@@ -643,16 +643,18 @@ int alloc(T** p, size_t count) {
 }
 
 // IMENV_STORE_DEFAULT: the state rows are written through as well when a launch's observation and
-// reward bytes fit the 32 MiB of L2 (8 XCDs x 4 MiB): then nearly every line a launch writes would
-// still be dirty at its end and the dependent-launch boundary would write it back (+ bytes / 6 TB/s,
-// MI355X_MICROARCH.md); larger launches evict their lines during the launch anyway, and there a state
-// row written through (a 64-byte ring row per wave: partial lines) costs more than it saves
-// (profiles/r03/).
-// IMENV_WT_STATE_MAX_BYTES overrides the 32 MiB limit (read once; tuning sweeps).
+// reward bytes are at most 24 MiB (L2 is 8 XCDs x 4 MiB): then nearly every line a launch writes
+// would still be dirty at its end and the dependent-launch boundary would write it back (+ bytes /
+// 6 TB/s, MI355X_MICROARCH.md); larger launches evict their lines during the launch anyway, and there
+// a state row written through (a 64-byte ring row per wave: partial lines) costs more than it saves.
+// Measured (profiles/r03/store_sweep): state rows written through are 4-20% faster for C2 at 131,072 /
+// 262,144 envs (7.3 / 14.7 MB of outputs) and C4 at 131,072 (13.6 MB), 2-9% slower for C2 at 2^19 /
+// 2^20 (29 / 59 MB) and C3 at 262,144 (27 MB).
+// IMENV_WT_STATE_MAX_BYTES overrides the 24 MiB limit (read once; tuning sweeps).
 int64_t wt_state_limit() {
   static const int64_t lim = [] {
     const char* v = std::getenv("IMENV_WT_STATE_MAX_BYTES");
-    return v ? (int64_t)std::atoll(v) : (int64_t(32) << 20);
+    return v ? (int64_t)std::atoll(v) : (int64_t(24) << 20);
   }();
   return lim;
 }

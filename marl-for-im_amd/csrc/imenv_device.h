@@ -65,6 +65,12 @@ typedef unsigned long long uint64_t;
 #ifndef IMENV_STAMPS
 #define IMENV_STAMPS 0       // 1 (diagnostic builds only): per-wave phase timestamps into StepArgs::stamps
 #endif
+// Ablations (diagnostic builds only, WRONG results: timing where the compute goes): bit 0 skips the
+// divergent split, bit 1 the demand draw (Philox + Poisson), bit 2 computes observations as (float)v,
+// bit 3 skips profit / reward arithmetic, bit 4 skips the order decode (order = 0).
+#ifndef IMENV_ABLATE
+#define IMENV_ABLATE 0
+#endif
 #define IMENV_GUIDE_BITS 10
 
 namespace imenv {
@@ -104,11 +110,17 @@ __device__ __forceinline__ void wt_store8(__amdgpu_buffer_rsrc_t r, int off, dou
   __builtin_memcpy(&w, &v, 8);
   __builtin_amdgcn_raw_buffer_store_b64(w, r, off, 0, CPOL_SC1);
 }
-// a value every lane of the wave holds (e.g. the block's first env), as a scalar
+// a value every lane of the wave holds (e.g. the block's first env), as a scalar: a buffer resource
+// built from it stays in SGPRs (from a value the compiler cannot prove uniform it would emit a
+// readfirstlane waterfall loop around every buffer store)
 __device__ __forceinline__ int64_t uniform_i64(int64_t x) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
   return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  return reinterpret_cast<T*>(uniform_i64(reinterpret_cast<int64_t>(p)));
 }
 
 struct SpecDev {
@@ -612,6 +624,14 @@ __device__ __forceinline__ void decode_orders(const P& p, const double (&x)[P::N
   const int N = p.N();
   const double a = p.a();
   const double bma = p.bma();
+  // A power-of-two 1 / (b - a) folds into order_max exactly: scaling by 2^k commutes with rounding, so
+  // (d * om) * 2^k == d * (om * 2^k) bit for bit while no product leaves the normal range, which holds
+  // when a is 0 or at least 2^-900 in magnitude (then x - a is 0 or >= 2^-953) and 2^k >= 2^-60.
+  // rescale's trailing "+ 0" (rev_scale, IM_env.py:446-456) only turns -0.0 into +0.0, which the clip
+  // and the integer conversion below ignore, so it is dropped. Every step is checked against the
+  // reference's golden vectors and the oracle (tests/test_gpu_parity.py, tests/test_fuzz_gpu.py).
+  const double ib = p.inv_bma();
+  const bool fold = ib >= 0x1p-60 && (a == 0.0 || fabs(a) >= 0x1p-900);
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     order[i] = 0;
@@ -619,11 +639,11 @@ __device__ __forceinline__ void decode_orders(const P& p, const double (&x)[P::N
       const double om = (double)p.order_max(i);
       double v = x[i];
       if (p.std_actions()) {
-        const double q = (x[i] - a) * (om - 0.0);
-        v = (p.inv_bma() != 0.0 ? q * p.inv_bma() : q / bma) + 0.0;
+        const double d = x[i] - a;
+        v = fold ? d * (om * ib) : (ib != 0.0 ? (d * om) * ib : (d * om) / bma);
       }
       const double o = p.clip_round() ? rint(fmin(fmax(v, 0.0), om)) : fmin(fmax(rint(v), 0.0), om);
-      order[i] = (int)o;
+      order[i] = (IMENV_ABLATE & 16) ? 0 : (int)o;
     }
   }
 }
@@ -678,7 +698,7 @@ __device__ __forceinline__ void step_core(const P& p, const int t, const int (&o
     }
   }
   split_ok = true;
-  if constexpr (MC > 0) {
+  if constexpr (MC > 0 && !(IMENV_ABLATE & 1)) {
 #pragma unroll
     for (int si = 0; si < NT; ++si) {
       if (si >= p.num_split()) break;
@@ -709,7 +729,10 @@ __device__ __forceinline__ void step_core(const P& p, const int t, const int (&o
       for (int k = 0; k < MC; ++k) x1[k] = caseD ? oc[k] + bto[k] : bto[k];
       int amt = caseB ? 0 : shp;
       const int lim1 = caseA ? p.split_limit(q, 0) : (caseD ? p.split_limit(q, 3) : p.split_limit(q, 2));
-      bool ok = rr_closed<MC>(m, x1, s, amt, lim1, !caseD);
+      // a lane with nothing to ship (amt <= 0) leaves the loop at once with x1, s and amt unchanged
+      // (rounds 0 <= limit): when that holds for the whole wave, the loop is skipped (wave-uniform)
+      bool ok = true;
+      if (__builtin_amdgcn_ballot_w64(amt > 0) != 0) ok = rr_closed<MC>(m, x1, s, amt, lim1, !caseD);
       if (!caseD) {
 #pragma unroll
         for (int k = 0; k < MC; ++k) bto[k] = x1[k];   // A and C drain backlog_to in place
@@ -719,7 +742,7 @@ __device__ __forceinline__ void step_core(const P& p, const int t, const int (&o
 #pragma unroll
       for (int k = 0; k < MC; ++k) out[k] = oc[k];
       int amt2 = second ? amt : 0;
-      ok = rr_closed<MC>(m, out, s, amt2, p.split_limit(q, 1), true) && ok;
+      if (__builtin_amdgcn_ballot_w64(second) != 0) ok = rr_closed<MC>(m, out, s, amt2, p.split_limit(q, 1), true) && ok;
 #pragma unroll
       for (int k = 0; k < MC; ++k) {
         if (second) bto[k] += out[k];
@@ -751,6 +774,7 @@ __device__ __forceinline__ void step_core(const P& p, const int t, const int (&o
       const int im = p.inv_max(i);
       const int ou2 = min(max(ou[i] + order[i] - acq[i], 0), im);
       const int inv2 = min(max(inv[i] + acq[i] - ship[i], 0), im);
+      if constexpr (IMENV_ABLATE & 8) prof[i] = (double)(ship[i] - order[i]); else
       prof[i] = ((p.sell(i) * (double)ship[i] - p.buy(i) * (double)order[i]) -
                  p.stock_cost(i) * fabs((double)inv2 - p.inv_target(i))) -
                 p.backlog_cost(i) * (double)b2;
@@ -1024,7 +1048,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
         if (p.demand_layout() == IMENV_LAYOUT_DRAW) {
           const uint32_t w = rng_word(gid, ep, t, STREAM_DEMAND, r, k0, k1);
           if (poisson) {
-            cdraw[i] = p.poisson_draw(w, s_tab);
+            cdraw[i] = (IMENV_ABLATE & 2) ? 5 : p.poisson_draw(w, s_tab);
           } else {
             const uint64_t rng = (uint64_t)(p.uniform_high() - p.uniform_low());
             cdraw[i] = p.uniform_low() + (int)(((uint64_t)w * rng) >> 32);
@@ -1391,7 +1415,7 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           if ((total & 1) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0) {
             double2* g2 = reinterpret_cast<double2*>(gobs);
             if constexpr (IMENV_WT_STORE) {
-              const auto rs = wt_rsrc(gobs);
+              const auto rs = wt_rsrc(uniform_ptr(gobs));
               for (int q = gl; q < total / 2; q += GS) wt_store16(rs, q * 16, make_double2(at(so, 2 * q), at(so, 2 * q + 1)));
             } else {
               for (int q = gl; q < total / 2; q += GS)
@@ -1419,7 +1443,7 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           if ((total & 3) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0) {
             float4* g4 = reinterpret_cast<float4*>(gobs);
             if constexpr (IMENV_WT_STORE) {
-              const auto rs = wt_rsrc(gobs);
+              const auto rs = wt_rsrc(uniform_ptr(gobs));
               if constexpr (SSTR == row) {
                 const float4* s4 = reinterpret_cast<const float4*>(so);
                 for (int q = gl; q < total / 4; q += GS) wt_store16(rs, q * 16, s4[q]);

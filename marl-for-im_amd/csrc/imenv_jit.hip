@@ -162,10 +162,29 @@ void emit_obs_hooks(std::ostream& o, const SpecDev& d) {
         else full = false;
       }
       if (!full) hi = mx;
-      bool k1 = true, k2 = true, k3 = true, q1 = true, q2 = true;
+      // k4: all-float32 correctly rounded division of the integer numerator m = v * (b - a) + a * den by den
+      // (one Newton-Markstein correction), when a, b - a and den are integers and |m| stays below 2^24
+      const double den = s.group_den[g][i];
+      const bool ints = s.a == std::floor(s.a) && (s.b - s.a) == std::floor(s.b - s.a) && den == std::floor(den) &&
+                        den >= 1.0 && den < 16777216.0 && std::fabs(s.a) < 65536.0 && std::fabs(s.b - s.a) < 65536.0;
+      const long long B4 = ints ? (long long)(s.b - s.a) : 0, A4 = ints ? (long long)(s.a * den) : 0;
+      const float rc4 = (float)(1.0 / den), den4 = (float)den;
+      bool k1 = true, k2 = true, k3 = true, k4 = ints, q1 = true, q2 = true, q3 = den != 0.0 && std::isfinite(den);
+      const double rc64 = 1.0 / den;
       for (int64_t v = 0; v <= hi; ++v) {
         const double e = ref_obs(s, g, i, (int)v);
         const float e32 = (float)e;
+        if (k4) {
+          const long long m = v * B4 + A4;
+          if (m <= -16777216 || m >= 16777216) {
+            k4 = false;
+          } else {
+            const float mf = (float)m;
+            const float q0 = mf * rc4;
+            const float r4 = std::fmaf(std::fmaf(-q0, den4, mf), rc4, q0);
+            k4 = std::memcmp(&r4, &e32, 4) == 0;
+          }
+        }
         const float r1 = std::fmaf((float)v, c1, c0);
         const float r2 = (float)std::fma((double)v, d1, s.a);
         const float r3 = (float)((double)v * d1 + s.a);
@@ -176,6 +195,12 @@ void emit_obs_hooks(std::ostream& o, const SpecDev& d) {
         const double s2 = (double)v * d1 + s.a;
         q1 = q1 && std::memcmp(&s1, &e, 8) == 0;
         q2 = q2 && std::memcmp(&s2, &e, 8) == 0;
+        if (q3) {   // the reference expression with its division by one Newton-Markstein correction
+          const double tv = clamp ? std::fmin((double)v, clip) * (s.b - s.a) : (double)v * (s.b - s.a);
+          const double t0 = tv * rc64;
+          const double s3 = s.a + std::fma(std::fma(-t0, den, tv), rc64, t0);
+          q3 = std::memcmp(&s3, &e, 8) == 0;
+        }
       }
       // guard (partial verification) or clamp (clamped group verified up to its integral clip)
       std::string pre;
@@ -190,15 +215,24 @@ void emit_obs_hooks(std::ostream& o, const SpecDev& d) {
                                  dlit(s.b - s.a) + ", " + dlit(s.group_den[g][i]) + ", " +
                                  dlit(s.group_clip[g][i]) + ")";
       if (k1) c32 << cs << pre << ret << "__builtin_fmaf((float)v, " << flit(c1) << ", " << flit(c0) << ")" << tail;
+      else if (k4)
+        c32 << cs << pre << "{ const float m = (float)(v * " << B4 << " + (" << A4 << ")); const float q0 = m * "
+            << flit(rc4) << "; return __builtin_fmaf(__builtin_fmaf(-q0, " << flit(den4) << ", m), " << flit(rc4)
+            << ", q0); }" << (full ? "\n" : " break;\n");
       else if (k2) c32 << cs << pre << ret << "(float)__builtin_fma((double)v, " << dlit(d1) << ", " << dlit(s.a) << ")" << tail;
       else if (k3) c32 << cs << pre << ret << "(float)((double)v * " << dlit(d1) << " + " << dlit(s.a) << ")" << tail;
       else c32 << cs << "return (float)" << direct << ";\n";
       if (q1) c64 << cs << pre << ret << "__builtin_fma((double)v, " << dlit(d1) << ", " << dlit(s.a) << ")" << tail;
       else if (q2) c64 << cs << pre << ret << "(double)v * " << dlit(d1) << " + " << dlit(s.a) << tail;
+      else if (q3)
+        c64 << cs << pre << "{ const double tv = (double)v * " << dlit(s.b - s.a) << "; const double t0 = tv * " << dlit(rc64)
+            << "; return " << dlit(s.a) << " + __builtin_fma(__builtin_fma(-t0, " << dlit(den) << ", tv), " << dlit(rc64)
+            << ", t0); }" << (full ? "\n" : " break;\n");
       else c64 << cs << "return " << direct << ";\n";
     }
   }
   o << "  __device__ float obs32(int g, int i, int v, const float* __restrict__ lut) const {\n"
+       "#if (IMENV_ABLATE & 4)\n    return (float)v;   // diagnostic ablation (imenv_device.h)\n#endif\n"
        "    switch (g * 256 + i) {\n"
     << c32.str()
     << "    default: break;\n    }\n    return imenv::obs_value32(*this, lut, g, i, v);\n  }\n";

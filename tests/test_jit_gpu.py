@@ -191,3 +191,20 @@ def test_gpu_rollout_stepper_matches_step(name, odt, rows):
     r = r[..., None] if r.ndim == 2 else r
     np.testing.assert_array_equal(np.transpose(r, (1, 0, 2)), d["reward"][..., :r.shape[-1]])
     env.close()
+
+
+@pytest.mark.parametrize("cfg,n,flags", [("C4", 131072, 0x6000), ("C3", 262144, 0x2000), ("C2", 1 << 20, 0x2000),
+                                         ("C2", 262144, 0x6000)])
+def test_default_store_policy_by_batch_size(cfg, n, flags):
+    """IMENV_STORE_DEFAULT writes observations / rewards through at every size and the state rows too
+    only while a launch's observation + reward bytes stay within 24 MiB (C4 at 131,072 envs: 13.6 MB;
+    C2 at 262,144: 14.7 MB; not C3 at 262,144: 27.3 MB, nor C2 at 2^20: 58.7 MB)."""
+    import bench
+    from imenv import VectorInvEnv
+    kind, c = bench.CONFIGS[cfg][:2]
+    env = VectorInvEnv(kind, c, n_envs=n, device=DEV)
+    env.reset()
+    env.step(torch.zeros((n, env.N), device=DEV))
+    got = int(re.search(r"flags=0x([0-9a-f]+)", env.kernel_info()).group(1), 16)
+    assert got & 0x6800 == flags, env.kernel_info()
+    env.close()
