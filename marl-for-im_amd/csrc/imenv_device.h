@@ -71,6 +71,9 @@ typedef unsigned long long uint64_t;
 #ifndef IMENV_ABLATE
 #define IMENV_ABLATE 0
 #endif
+#ifndef IMENV_PRIO
+#define IMENV_PRIO 0         // > 0: waves in odd hardware slots of a SIMD raise their issue priority (stagger)
+#endif
 #define IMENV_GUIDE_BITS 10
 
 namespace imenv {
@@ -279,6 +282,39 @@ __device__ __forceinline__ int ceil_div_pos(int a, int b) {
 // branch of the split runs this one loop (no divergent copies of it in a wave).
 template <int MC>
 __device__ __forceinline__ bool rr_closed(int m, int (&x)[MC], int (&s)[MC], int& amt, int lim, bool sumcheck) {
+  if constexpr (MC == 2) {
+    // Two children (m == 2: a split needs two): the phases below run straight-line, each masked by
+    // `live` instead of leaving a loop, so a wave pays three phases of arithmetic instead of looping
+    // until its slowest lane is done. Three suffice: a phase that keeps both children eligible ends
+    // with amt <= 0 (r = ceil(amt / 2)) or at the guard, since ceil(S / 2) >= mn when both are
+    // positive; otherwise a child's count reaches 0 and the next phase has one eligible child, which
+    // ends with its count, amt or S at 0 or at the guard; the third phase can then only stop or trip
+    // the guard (nothing eligible while amt > 0 without the sum check).
+    int rounds = 0;
+    bool live = true;
+#pragma unroll
+    for (int ph = 0; ph < 3; ++ph) {
+      const int S = x[0] + x[1];
+      const bool e0 = x[0] > 0, e1 = x[1] > 0;
+      const int cnt = (int)e0 + (int)e1;
+      const int mn = e0 ? (e1 ? min(x[0], x[1]) : x[0]) : x[1];
+      const bool stop = amt <= 0 || (sumcheck && S <= 0);
+      const bool trip = !stop && cnt == 0;
+      if (live && trip) rounds = lim + 1;
+      live = live && !stop && !trip;
+      const int c1 = cnt > 1 ? 2 : 1;
+      int r = min(mn, ceil_div_pos(amt, c1));
+      if (sumcheck) r = min(r, ceil_div_pos(S, c1));
+      r = min(r, lim + 1 - rounds);
+      if (!live) r = 0;
+      if (e0) { x[0] -= r; s[0] += r; }
+      if (e1) { x[1] -= r; s[1] += r; }
+      amt -= r * cnt;
+      rounds += r;
+      live = live && rounds <= lim;
+    }
+    return rounds <= lim;
+  }
   int rounds = 0;
 #pragma unroll 1
   for (int ph = 0; ph <= MC + 1; ++ph) {
@@ -1367,6 +1403,13 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   // 6 stores acknowledged
   [[maybe_unused]] uint64_t stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if constexpr (IMENV_STAMPS) stamp[0] = __builtin_amdgcn_s_memrealtime();
+  if constexpr (IMENV_PRIO > 0) {
+    // Two waves per SIMD run the same phases in lockstep (load, compute, store). With one of them at a
+    // higher issue priority it finishes its arithmetic first and its stores overlap the other's
+    // arithmetic (MI355X_MICROARCH.md, "Two waves per SIMD", item 4). HW_ID bits 3:0 = wave slot.
+    const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (3 << 11));
+    if (hw & 1u) __builtin_amdgcn_s_setprio(IMENV_PRIO);
+  }
   StepLoad<P> L[EPT];
 #pragma unroll
   for (int k = 0; k < EPT; ++k) step_load(p, A, eb + k * BS + tid, L[k]);
