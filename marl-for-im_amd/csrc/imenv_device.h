@@ -74,6 +74,12 @@ typedef unsigned long long uint64_t;
 #ifndef IMENV_PRIO
 #define IMENV_PRIO 0         // > 0: waves in odd hardware slots of a SIMD raise their issue priority (stagger)
 #endif
+#ifndef IMENV_BUF_LOAD
+#define IMENV_BUF_LOAD 0     // 1: exact-row step loads as buffer loads off the block's first env (SGPR bases)
+#endif
+#ifndef IMENV_SLAB_BATCH
+#define IMENV_SLAB_BATCH 1   // 1: a whole group's observation slab is written out in batches of LDS reads
+#endif
 #define IMENV_GUIDE_BITS 10
 
 namespace imenv {
@@ -283,37 +289,32 @@ __device__ __forceinline__ int ceil_div_pos(int a, int b) {
 template <int MC>
 __device__ __forceinline__ bool rr_closed(int m, int (&x)[MC], int (&s)[MC], int& amt, int lim, bool sumcheck) {
   if constexpr (MC == 2) {
-    // Two children (m == 2: a split needs two): the phases below run straight-line, each masked by
-    // `live` instead of leaving a loop, so a wave pays three phases of arithmetic instead of looping
-    // until its slowest lane is done. Three suffice: a phase that keeps both children eligible ends
-    // with amt <= 0 (r = ceil(amt / 2)) or at the guard, since ceil(S / 2) >= mn when both are
-    // positive; otherwise a child's count reaches 0 and the next phase has one eligible child, which
-    // ends with its count, amt or S at 0 or at the guard; the third phase can then only stop or trip
-    // the guard (nothing eligible while amt > 0 without the sum check).
-    int rounds = 0;
-    bool live = true;
-#pragma unroll
-    for (int ph = 0; ph < 3; ++ph) {
-      const int S = x[0] + x[1];
-      const bool e0 = x[0] > 0, e1 = x[1] > 0;
-      const int cnt = (int)e0 + (int)e1;
-      const int mn = e0 ? (e1 ? min(x[0], x[1]) : x[0]) : x[1];
-      const bool stop = amt <= 0 || (sumcheck && S <= 0);
-      const bool trip = !stop && cnt == 0;
-      if (live && trip) rounds = lim + 1;
-      live = live && !stop && !trip;
-      const int c1 = cnt > 1 ? 2 : 1;
-      int r = min(mn, ceil_div_pos(amt, c1));
-      if (sumcheck) r = min(r, ceil_div_pos(S, c1));
-      r = min(r, lim + 1 - rounds);
-      if (!live) r = 0;
-      if (e0) { x[0] -= r; s[0] += r; }
-      if (e1) { x[1] -= r; s[1] += r; }
-      amt -= r * cnt;
-      rounds += r;
-      live = live && rounds <= lim;
-    }
-    return rounds <= lim;
+    // Two children (m == 2: a split needs two), straight-line, two phases and the guard:
+    //  1. both eligible: each round moves 2 units, r1 = min(x0, x1, ceil(amt / 2)) rounds (with the
+    //     sum check, ceil(S / 2) >= min(x0, x1) never binds). amt may end at -1 (the reference's
+    //     inner loop does not re-check amt).
+    //  2. at most one eligible child c left: one unit per round, r2 = min(x_c, amt[, S]) (the other
+    //     child's count is <= 0, so with the sum check S = x_c + x_other stops it first). After it,
+    //     amt <= 0, S <= 0, or nothing is eligible: the loop ends, or without the sum check (the
+    //     capped loop, IM_div_env.py:488-498) spins until its guard trips.
+    // Rounds are capped at lim + 1 (the guard, IM_div_env.py:424-498) as the loop would be.
+    // Equal to the literal loop on every (x0, x1, amt, lim, sumcheck) with x in [-4, 13], amt in
+    // [-2, 31] and 8 guard limits (tools/check_rr_closed.py).
+    const bool go1 = amt > 0 && (!sumcheck || x[0] + x[1] > 0);
+    int r1 = min(min(min(x[0], x[1]), (amt + 1) >> 1), lim + 1);
+    if (!(go1 && x[0] > 0 && x[1] > 0)) r1 = 0;
+    x[0] -= r1; x[1] -= r1; s[0] += r1; s[1] += r1;
+    amt -= 2 * r1;
+    const bool e0 = x[0] > 0, e1 = x[1] > 0;
+    const bool go2 = go1 && amt > 0 && r1 <= lim;
+    int r2 = min(e0 ? x[0] : (e1 ? x[1] : 0), amt);
+    if (sumcheck) r2 = min(r2, x[0] + x[1]);
+    r2 = min(r2, lim + 1 - r1);
+    r2 = go2 ? max(r2, 0) : 0;
+    if (e0) { x[0] -= r2; s[0] += r2; } else if (e1) { x[1] -= r2; s[1] += r2; }
+    amt -= r2;
+    const bool trip = go2 && !sumcheck && amt > 0;
+    return r1 + r2 <= lim && !trip;
   }
   int rounds = 0;
 #pragma unroll 1
@@ -381,6 +382,49 @@ __device__ __forceinline__ void load_words(const void* __restrict__ p, uint32_t 
   } else {
 #pragma unroll
     for (int q = 0; q < W; ++q) w[q] = reinterpret_cast<const uint32_t*>(p)[q];
+  }
+}
+
+// load_words from a buffer resource at byte offset off (lanes past the resource's range read 0)
+template <int BYTES>
+__device__ __forceinline__ void buf_load_words(__amdgpu_buffer_rsrc_t r, int off, uint32_t (&w)[BYTES / 4]) {
+  constexpr int W = BYTES / 4;
+  if constexpr (BYTES % 16 == 0) {
+#pragma unroll
+    for (int q = 0; q < W / 4; ++q) {
+      const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * q, 0, 0);
+      w[4 * q] = x[0]; w[4 * q + 1] = x[1]; w[4 * q + 2] = x[2]; w[4 * q + 3] = x[3];
+    }
+  } else if constexpr (BYTES % 8 == 0) {
+#pragma unroll
+    for (int q = 0; q < W / 2; ++q) {
+      const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, off + 8 * q, 0, 0);
+      w[2 * q] = x[0]; w[2 * q + 1] = x[1];
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < W; ++q) w[q] = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * q, 0, 0);
+  }
+}
+// a read-only resource over cnt elements of BYTES bytes from base (base and cnt wave-uniform)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ld_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+template <typename T>
+__device__ __forceinline__ T buf_load_elem(__amdgpu_buffer_rsrc_t r, int off) {
+  if constexpr (sizeof(T) == 1) return (T)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+  else if constexpr (sizeof(T) == 2) return (T)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+  else if constexpr (sizeof(T) == 4) {
+    const uint32_t x = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+    T v;
+    __builtin_memcpy(&v, &x, 4);
+    return v;
+  } else {
+    const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    T v;
+    __builtin_memcpy(&v, &x, 8);
+    return v;
   }
 }
 
@@ -810,10 +854,18 @@ __device__ __forceinline__ void step_core(const P& p, const int t, const int (&o
       const int im = p.inv_max(i);
       const int ou2 = min(max(ou[i] + order[i] - acq[i], 0), im);
       const int inv2 = min(max(inv[i] + acq[i] - ship[i], 0), im);
+      // With integral prices of at most 2^12 (JIT constants), 8-bit state (0 <= ship <= inv + acq <
+      // 2^8 + 2^15 with the int16 noisy-delay carry) and order_max < 2^16, sell * ship - buy * order
+      // is an integer below 2^29 in magnitude that float64 holds exactly, as it holds both products:
+      // the integer difference converted once is the reference's float64 difference bit for bit (one
+      // conversion instead of two conversions, two products and a sum).
+      const double sv = p.sell(i), bv = p.buy(i);
+      const bool int_rev = P::JIT && sizeof(typename P::ST) == 1 && p.order_max(i) < 65536 && sv == rint(sv) &&
+                           bv == rint(bv) && fabs(sv) <= 0x1p12 && fabs(bv) <= 0x1p12;
+      const double rev = int_rev ? (double)((int)sv * ship[i] - (int)bv * order[i])
+                                 : sv * (double)ship[i] - bv * (double)order[i];
       if constexpr (IMENV_ABLATE & 8) prof[i] = (double)(ship[i] - order[i]); else
-      prof[i] = ((p.sell(i) * (double)ship[i] - p.buy(i) * (double)order[i]) -
-                 p.stock_cost(i) * fabs((double)inv2 - p.inv_target(i))) -
-                p.backlog_cost(i) * (double)b2;
+      prof[i] = (rev - p.stock_cost(i) * fabs((double)inv2 - p.inv_target(i))) - p.backlog_cost(i) * (double)b2;
       bl[i] = b2; ou[i] = ou2; inv[i] = inv2;
       push[i] = (i == p.factory()) ? order[i] : sto[i];
     }
@@ -880,6 +932,29 @@ __device__ __forceinline__ void lds_row_store(float* __restrict__ s, const float
   }
 }
 // Whether this call's observations go through the slab (the slab's value type matches the call's).
+// Write-out of a whole group's slab: QT 16-byte words, word q = lane + k * GS. The reads of up to 8
+// words are issued before the first of their stores, so a lane waits for LDS once per batch (a loop
+// with a runtime trip count waits once per word: ~6 serialised LDS round trips for a 24-float row).
+template <int QT, int GS, class RQ, class WQ>
+__device__ __forceinline__ void slab_copy(const int gl, const RQ& rq, const WQ& wq) {
+  constexpr int K = (QT + GS - 1) / GS;
+  constexpr int B = 8;
+#pragma unroll
+  for (int k0 = 0; k0 < K; k0 += B) {
+    decltype(rq(0)) v[B];
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      const int q = gl + (k0 + j) * GS;
+      if (k0 + j < K && (QT % GS == 0 || q < QT)) v[j] = rq(q);
+    }
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      const int q = gl + (k0 + j) * GS;
+      if (k0 + j < K && (QT % GS == 0 || q < QT)) wq(q, v[j]);
+    }
+  }
+}
+
 template <class P>
 __device__ __forceinline__ bool staged_obs(const P& p) {
   return P::OBS_STAGE64 ? p.obs_f64() : !p.obs_f64();
@@ -948,7 +1023,60 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
   for (int q = 0; q < R32::WORDS; ++q) w_bto[q] = 0;
 #pragma unroll
   for (int i = 0; i < NT; ++i) { cdem[i] = 0; du[i] = 1.0; r_arr[i] = 0; }
-  {
+  if constexpr (IMENV_BUF_LOAD && EXACT) {
+    // buffer loads off the slab's first env: the bases are scalars, the lane's byte offset is shared by
+    // every row of one element size, and lanes past n read 0 (the resource ends at the last env), so
+    // no 64-bit address arithmetic and no tail clamp
+    const int lane = threadIdx.x;
+    const int64_t e0 = uniform_i64(e - lane);
+    const int64_t left = n - e0;
+    const uint32_t cnt = (uint32_t)(left < (int64_t)P::BS ? left : (int64_t)P::BS);
+    if (p.act_f64()) {
+      buf_load_words<8 * NT>(ld_rsrc(static_cast<const double*>(A.actions) + e0 * NT, cnt * 8 * NT), lane * 8 * NT, aw);
+    } else {
+      uint32_t (&a32)[NT] = *reinterpret_cast<uint32_t(*)[NT]>(aw);
+      buf_load_words<4 * NT>(ld_rsrc(static_cast<const float*>(A.actions) + e0 * NT, cnt * 4 * NT), lane * 4 * NT, a32);
+    }
+    buf_load_words<RN::BYTES>(ld_rsrc(p_net + e0 * RN::NPT, cnt * RN::BYTES), lane * RN::BYTES, w_net);
+    buf_load_words<R::BYTES>(ld_rsrc(p_ou + e0 * R::NPT, cnt * R::BYTES), lane * R::BYTES, w_ou);
+    constexpr int ES = (int)sizeof(ST);
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+      r_arr[i] = buf_load_elem<ST>(ld_rsrc(p_ring + (int64_t)A.ring_row[i] * n + e0, cnt * ES), lane * ES);
+    if (p.noisy_delay()) buf_load_words<RC::BYTES>(ld_rsrc(p_carry + e0 * RC::NPT, cnt * RC::BYTES), lane * RC::BYTES, w_cin);
+    if (MC > 0) buf_load_words<R32::BYTES>(ld_rsrc(p_bto + e0 * R32::NPT, cnt * R32::BYTES), lane * R32::BYTES, w_bto);
+    if (p.demand_layout() == IMENV_LAYOUT_PER_ENV) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const int r = p.retailer_slot(i);
+        if (r >= 0)
+          cdem[i] = buf_load_elem<int>(ld_rsrc(A.demand + ((int64_t)t * p.num_retailers() + r) * n + e0, cnt * 4), lane * 4);
+      }
+    }
+    if (p.has_delay_u()) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+        du[i] = buf_load_elem<double>(ld_rsrc(A.delay_u + ((int64_t)t * N + i) * n + e0, cnt * 8), lane * 8);
+    }
+    if constexpr (P::TD_PRE > 0) {   // (as below)
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+#pragma unroll
+        for (int j = 0; j < P::TD_PRE; ++j) {
+          L.r_td[i][j] = 0;
+          const int d = p.delay(i);
+          if (j < d - 1 && t + 1 + j - d >= 0)
+            L.r_td[i][j] = buf_load_elem<ST>(ld_rsrc(p_ring + (int64_t)(p.ring_off(i) + (t + 1 + j) % d) * n + e0, cnt * ES),
+                                             lane * ES);
+        }
+      }
+    }
+    if (p.has_metrics() && t > 0) {
+      const int64_t el = valid ? e : n - 1;
+#pragma unroll
+      for (int k = 0; k < 4 + NT; ++k) if (k < 4 + N) macc[k] = A.metrics[el * (4 + N) + k];
+    }
+  } else {
     // every lane loads (a tail lane re-reads the last env; only stores are guarded): no branch, so the
     // loads and the draws below share one basic block and the draws run under the loads' latency
     const int64_t el = valid ? e : n - 1;
@@ -1121,14 +1249,16 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   for (int i = 0; i < NT; ++i) arr[i] = (int)r_arr[i];
   RC::unpack(w_cin, cin);
   R32::unpack(w_bto, btoc);
+  if (t == 0) {              // period-0 state is implicit (IM_env.py:221-224); one uniform branch
 #pragma unroll
-  for (int i = 0; i < NT; ++i) {
-    if (t == 0) {            // period-0 state is implicit (IM_env.py:221-224)
+    for (int i = 0; i < NT; ++i) {
       inv[i] = (i < N) ? p.init_inv(i) : 0;
       bl[i] = ou[i] = cin[i] = btoc[i] = 0;
     }
-    if (i >= N || t < p.delay(i < N ? i : 0)) arr[i] = 0;   // nothing shipped d periods ago yet
   }
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+    if (i >= N || t < p.delay(i < N ? i : 0)) arr[i] = 0;   // nothing shipped d periods ago yet
 
   // per-period inputs that do not come from the state rows: customer demand (layout + noise) and
   // the noisy-delay deferral decision
@@ -1457,7 +1587,16 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           // 16-byte stores need a 16-byte aligned destination (a caller's obs_out view may be offset)
           if ((total & 1) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0) {
             double2* g2 = reinterpret_cast<double2*>(gobs);
-            if constexpr (IMENV_WT_STORE) {
+            if (IMENV_SLAB_BATCH && cnt == GS) {   // a whole group (as the float32 write-out below)
+              constexpr int QT = row * GS / 2;
+              auto rq = [&](int q) { return make_double2(at(so, 2 * q), at(so, 2 * q + 1)); };
+              if constexpr (IMENV_WT_STORE) {
+                const auto rs = wt_rsrc(uniform_ptr(gobs));
+                slab_copy<QT, GS>(gl, rq, [&](int q, const double2& v) { wt_store16(rs, q * 16, v); });
+              } else {
+                slab_copy<QT, GS>(gl, rq, [&](int q, const double2& v) { store16<IMENV_NT_STORE>(g2 + q, v); });
+              }
+            } else if constexpr (IMENV_WT_STORE) {
               const auto rs = wt_rsrc(uniform_ptr(gobs));
               for (int q = gl; q < total / 2; q += GS) wt_store16(rs, q * 16, make_double2(at(so, 2 * q), at(so, 2 * q + 1)));
             } else {
@@ -1485,7 +1624,24 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           const float* so = s_obs + k * SLAB + gi * GS * SSTR;
           if ((total & 3) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0) {
             float4* g4 = reinterpret_cast<float4*>(gobs);
-            if constexpr (IMENV_WT_STORE) {
+            // 16-byte word q of the group's contiguous output, read from the slab
+            auto rq = [&](int q) -> float4 {
+              if constexpr (SSTR == row) return reinterpret_cast<const float4*>(so)[q];
+              else if constexpr (row % 4 == 0 && SSTR % 4 == 0)   // (q / R) * SSTR + (q % R) * 4, R = row / 4
+                return *reinterpret_cast<const float4*>(so + 4 * q + (SSTR - row) * (q / (row / 4)));
+              else return make_float4(at(so, 4 * q), at(so, 4 * q + 1), at(so, 4 * q + 2), at(so, 4 * q + 3));
+            };
+            if (IMENV_SLAB_BATCH && cnt == GS) {
+              // a whole group: QT words at compile time, every LDS read of a batch issued before its
+              // first store (one LDS wait per batch instead of one per word)
+              constexpr int QT = row * GS / 4;
+              if constexpr (IMENV_WT_STORE) {
+                const auto rs = wt_rsrc(uniform_ptr(gobs));
+                slab_copy<QT, GS>(gl, rq, [&](int q, const float4& v) { wt_store16(rs, q * 16, v); });
+              } else {
+                slab_copy<QT, GS>(gl, rq, [&](int q, const float4& v) { store16<IMENV_NT_STORE>(g4 + q, v); });
+              }
+            } else if constexpr (IMENV_WT_STORE) {
               const auto rs = wt_rsrc(uniform_ptr(gobs));
               if constexpr (SSTR == row) {
                 const float4* s4 = reinterpret_cast<const float4*>(so);
