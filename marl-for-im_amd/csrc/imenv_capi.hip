@@ -900,7 +900,7 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
   A.noisy_delay_thr = h->noisy_thr;
   A.noisy_delay_thr32 = prob_thr32(h->noisy_thr);
   A.noisy_demand_thr32 = prob_thr32(s.noisy_demand_threshold);
-  for (int i = 0; i < s.num_nodes; ++i) A.ring_row[i] = h->host.ring_off[i] + h->t % s.delay[i];
+  for (int i = 0; i < s.num_nodes; ++i) A.ring_at[i] = (int64_t)(h->host.ring_off[i] + h->t % s.delay[i]) * h->n;
   LaunchCfg c;
   c.mc = h->maxc;
   c.base = is_base_obs(s);

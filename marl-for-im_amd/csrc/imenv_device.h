@@ -196,7 +196,7 @@ struct StepArgs {
   double noisy_delay_thr;
   uint64_t noisy_delay_thr32;
   uint64_t noisy_demand_thr32;
-  int32_t ring_row[IMENV_MAX_NODES];  // ring_off[i] + t mod delay[i]
+  int64_t ring_at[IMENV_MAX_NODES];   // element offset of node i's ring row this step: (ring_off[i] + t mod delay[i]) * n
 };
 
 // Fused base-stock rollout (imenv_base_stock_rollout): whole episodes of P policies x S demand
@@ -311,7 +311,9 @@ __device__ __forceinline__ bool rr_closed(int m, int (&x)[MC], int (&s)[MC], int
     if (sumcheck) r2 = min(r2, x[0] + x[1]);
     r2 = min(r2, lim + 1 - r1);
     r2 = go2 ? max(r2, 0) : 0;
-    if (e0) { x[0] -= r2; s[0] += r2; } else if (e1) { x[1] -= r2; s[1] += r2; }
+    const int r2a = e0 ? r2 : 0, r2b = r2 - r2a;   // r2 == 0 when neither child is eligible: no branches
+    x[0] -= r2a; s[0] += r2a;
+    x[1] -= r2b; s[1] += r2b;
     amt -= r2;
     const bool trip = go2 && !sumcheck && amt > 0;
     return r1 + r2 <= lim && !trip;
@@ -1042,7 +1044,7 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
     constexpr int ES = (int)sizeof(ST);
 #pragma unroll
     for (int i = 0; i < NT; ++i)
-      r_arr[i] = buf_load_elem<ST>(ld_rsrc(p_ring + (int64_t)A.ring_row[i] * n + e0, cnt * ES), lane * ES);
+      r_arr[i] = buf_load_elem<ST>(ld_rsrc(p_ring + A.ring_at[i] + e0, cnt * ES), lane * ES);
     if (p.noisy_delay()) buf_load_words<RC::BYTES>(ld_rsrc(p_carry + e0 * RC::NPT, cnt * RC::BYTES), lane * RC::BYTES, w_cin);
     if (MC > 0) buf_load_words<R32::BYTES>(ld_rsrc(p_bto + e0 * R32::NPT, cnt * R32::BYTES), lane * R32::BYTES, w_bto);
     if (p.demand_layout() == IMENV_LAYOUT_PER_ENV) {
@@ -1065,9 +1067,11 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
         for (int j = 0; j < P::TD_PRE; ++j) {
           L.r_td[i][j] = 0;
           const int d = p.delay(i);
-          if (j < d - 1 && t + 1 + j - d >= 0)
-            L.r_td[i][j] = buf_load_elem<ST>(ld_rsrc(p_ring + (int64_t)(p.ring_off(i) + (t + 1 + j) % d) * n + e0, cnt * ES),
-                                             lane * ES);
+          if (j < d - 1) {   // loaded at every period (a valid ring row), used from t = d - 1 - j on
+            const ST v = buf_load_elem<ST>(ld_rsrc(p_ring + (int64_t)(p.ring_off(i) + (t + 1 + j) % d) * n + e0, cnt * ES),
+                                           lane * ES);
+            L.r_td[i][j] = (t + 1 + j - d >= 0) ? v : (ST)0;
+          }
         }
       }
     }
@@ -1105,7 +1109,7 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
     R::load(p_ou, el, np, N, w_ou);
 #pragma unroll
     for (int i = 0; i < NT; ++i)
-      if (i < N) r_arr[i] = p_ring[(int64_t)A.ring_row[i] * n + el];
+      if (i < N) r_arr[i] = p_ring[A.ring_at[i] + el];
     if (p.noisy_delay()) RC::load(p_carry, el, np, N, w_cin);
     if (MC > 0) R32::load(p_bto, el, np, N, w_bto);
     if (p.demand_layout() == IMENV_LAYOUT_PER_ENV) {
@@ -1130,8 +1134,12 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
           L.r_td[i][j] = 0;
           if (i < N) {
             const int d = p.delay(i);
-            if (j < d - 1 && t + 1 + j - d >= 0)
-              L.r_td[i][j] = p_ring[(int64_t)(p.ring_off(i) + (t + 1 + j) % d) * n + el];
+            // loaded at every period (a valid ring row), used from t = d - 1 - j on: no branch around the
+            // load, so the kernel's argument loads and all of its state loads form one block
+            if (j < d - 1) {
+              const ST v = p_ring[(int64_t)(p.ring_off(i) + (t + 1 + j) % d) * n + el];
+              L.r_td[i][j] = (t + 1 + j - d >= 0) ? v : (ST)0;
+            }
           }
         }
       }
@@ -1305,7 +1313,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
       R::store_wt(p_ou, e0, tid, ou);
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
-        const auto rr = wt_rsrc(p_ring + (int64_t)A.ring_row[i] * n + e0);
+        const auto rr = wt_rsrc(p_ring + A.ring_at[i] + e0);
         if constexpr (sizeof(ST) == 1) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)push[i], rr, tid, 0, CPOL_SC1);
         else if constexpr (sizeof(ST) == 2) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)push[i], rr, 2 * tid, 0, CPOL_SC1);
         else __builtin_amdgcn_raw_buffer_store_b32((uint32_t)push[i], rr, 4 * tid, 0, CPOL_SC1);
@@ -1317,7 +1325,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
       R::store(p_ou, e, np, N, ou);
 #pragma unroll
       for (int i = 0; i < NT; ++i)
-        if (i < N) p_ring[(int64_t)A.ring_row[i] * n + e] = (ST)push[i];
+        if (i < N) p_ring[A.ring_at[i] + e] = (ST)push[i];
       if (p.noisy_delay()) RC::store(p_carry, e, np, N, cout);
       if (MC > 0) R32::store(p_bto, e, np, N, btoc);
     }

@@ -46,12 +46,12 @@ def closed(x, s, amt, lim, sumcheck):
         r2 = min(r2, x0 + x1)
     r2 = min(r2, lim + 1 - r1)
     r2 = max(r2, 0) if go2 else 0
-    if e0:
-        x0 -= r2
-        s0 += r2
-    elif e1:
-        x1 -= r2
-        s1 += r2
+    r2a = r2 if e0 else 0
+    r2b = r2 - r2a
+    x0 -= r2a
+    s0 += r2a
+    x1 -= r2b
+    s1 += r2b
     amt -= r2
     trip = go2 and not sumcheck and amt > 0
     return [x0, x1], [s0, s1], amt, (r1 + r2 <= lim and not trip)
