@@ -651,6 +651,10 @@ int alloc(T** p, size_t count) {
 // 262,144 envs (7.3 / 14.7 MB of outputs) and C4 at 131,072 (13.6 MB), 2-9% slower for C2 at 2^19 /
 // 2^20 (29 / 59 MB) and C3 at 262,144 (27 MB).
 // IMENV_WT_STATE_MAX_BYTES overrides the 24 MiB limit (read once; tuning sweeps).
+// at most two waves per SIMD (256 CUs x 4 SIMDs x 64 lanes x 2): the JIT step kernel then uses 64-env
+// blocks (JitFlags::small_blocks, imenv_jit.hip jit_step_block_size)
+constexpr int64_t kSmallLaunchEnvs = 2 * 64 * 4 * 256;
+
 int64_t wt_state_limit() {
   static const int64_t lim = [] {
     const char* v = std::getenv("IMENV_WT_STATE_MAX_BYTES");
@@ -921,6 +925,7 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
     f.wt_obs = h->store_policy == IMENV_STORE_DEFAULT || h->store_policy == IMENV_STORE_WRITETHROUGH;
     f.wt_state = h->store_policy == IMENV_STORE_WRITETHROUGH ||
                  (h->store_policy == IMENV_STORE_DEFAULT && wt_state_pays(s, h->n, A.obs_f64 != 0));
+    f.small_blocks = h->n <= kSmallLaunchEnvs;
     auto it = h->jit_k.find(f.key());
     if (it == h->jit_k.end()) {
       // compiling + loading a module is not stream work: never do it while the stream is being
@@ -1402,6 +1407,7 @@ int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, cha
   f.stream_store = flags & 2048u;
   f.wt_obs = flags & 8192u;
   f.wt_state = flags & 16384u;
+  f.small_blocks = flags & 32768u;
   f.demand_layout = (int)((flags >> 5) & 31u);
   std::string msg;
   std::string src;

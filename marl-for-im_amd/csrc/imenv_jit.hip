@@ -92,8 +92,12 @@ int64_t slab_bytes(const SpecDev& d, bool base, int bs, int vbytes, int ept) {
   return (int64_t)bs * ept * staged_stride(staged_row(d, base), vbytes) * vbytes;
 }
 
-int jit_step_block_size(const SpecDev& d, bool base, int vbytes, int ept) {
-  int bs = jit_block_size();
+// small: the handle's launch has at most two waves per SIMD (JitFlags::small_blocks). One generation
+// of waves then runs load, compute and store in lockstep; 64-env blocks (one wave, no slab barrier
+// across waves) measured 5.94 -> 5.78 us for C4 at 131,072 envs and 4.32 -> 4.26 us for C2 at
+// 131,072, while at 262,144+ envs they were slower (C3 +5%, C2 at 2^20 +4%; profiles/r03/ab_blocks_*).
+int jit_step_block_size(const SpecDev& d, bool base, int vbytes, int ept, bool small = false) {
+  int bs = (small && !std::getenv("IMENV_JIT_BS")) ? 64 : jit_block_size();
   if (staged_row(d, base) > 0 && (base || !std::getenv("IMENV_JIT_BS")))
     while (bs > 64 && slab_bytes(d, base, bs, vbytes, ept) > kStageLds) bs /= 2;
   return bs;
@@ -386,7 +390,7 @@ static const char* jit_kernel_name(const JitFlags& f) {
 std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f) {
   std::ostringstream o;
   const int ept = jit_envs_per_thread(d, base, f.obs_f64);
-  emit_policy(o, d, maxc, base, f, jit_step_block_size(d, base, f.obs_f64 ? 8 : 4, ept), ept);
+  emit_policy(o, d, maxc, base, f, jit_step_block_size(d, base, f.obs_f64 ? 8 : 4, ept, f.small_blocks), ept);
   o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
     << jit_kernel_name(f) << "(const imenv::SpecDev* __restrict__ sp, const imenv::StepArgs A) {\n"
        "  __shared__ uint32_t s_tab[JitSpec::TAB_LDS];\n"
@@ -500,7 +504,7 @@ bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const st
   const std::string src = jit_source(d, maxc, base, f);
   if (!load_module(src, arch, jit_kernel_name(f), out, msg)) return false;
   out.ept = jit_envs_per_thread(d, base, f.obs_f64);
-  out.bs = jit_step_block_size(d, base, f.obs_f64 ? 8 : 4, out.ept);
+  out.bs = jit_step_block_size(d, base, f.obs_f64 ? 8 : 4, out.ept, f.small_blocks);
   char tag[160];
   // dev=: hash of the device-code header, so a profile of an older kernel body never matches this one
   std::snprintf(tag, sizeof tag, "jit:%s[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,ept=%d,%zuB,dev=%08x]",
