@@ -376,6 +376,38 @@ def main():
 
     per_t = env.step_traffic_per_period()
 
+    def lead_spin(W, K):
+        """GPU cycles of a busy-wait (torch.cuda._sleep) to enqueue ahead of the timed launches. Small
+        launches (C4 at 131,072 envs: ~5.6 us each) are shorter than the host's enqueue of one step
+        (~6 us of Python, ctypes and hipModuleLaunchKernel), so the GPU would idle between launches and
+        the event pairs would time the host's pace instead of the kernel's. A spin as long as the host
+        falls behind over the K steps lets the launches queue up, so the events time them back to back;
+        the wall-clock value is unchanged (the host paces the loop either way). When the host keeps
+        ahead (the metric's 2^20-env launches), no spin. Calibrated on two untimed episodes (the step
+        sequence stays aligned: 2T steps bring the handle back to the same period). Returns (cycles,
+        host us per step, GPU us per step)."""
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        e0.record(stream)
+        torch.cuda._sleep(200000)
+        e1.record(stream)
+        e1.synchronize()
+        us_per_cycle = e0.elapsed_time(e1) * 1e3 / 200000
+        n_cal = 2 * T
+        torch.cuda._sleep(int(3000 / us_per_cycle))       # 3 ms: longer than enqueueing n_cal steps
+        e0.record(stream)
+        h0 = time.perf_counter()
+        run(W, n_cal)
+        h = (time.perf_counter() - h0) * 1e6 / n_cal
+        e1.record(stream)
+        e1.synchronize()
+        g = e0.elapsed_time(e1) * 1e3 / n_cal
+        if h <= g:
+            return 0, h, g
+        return int(K * (h - g) * 1.25 / us_per_cycle), h, g
+
+    spin_info = {}
+
     def timed(W, K):
         """W untimed warmup steps (the first one resets), then exactly K timed steps of the same step
         sequence, so the timed region holds the resets at its episode boundaries. Returns (wall s,
@@ -384,6 +416,12 @@ def main():
         if W == 0:
             run(0, 1)     # no warmup asked for: one step outside the sequence builds the hipRTC kernel
         run(0, W)
+        spin = 0
+        if gather is None:
+            spin, h_us, g_us = lead_spin(W, K)
+            if not spin_info:      # the line's own timed region (not the informational alt-store run)
+                spin_info.update(host_us_per_step=round(h_us, 3), gpu_us_per_step_queued=round(g_us, 3),
+                                 lead_spin_cycles=spin)
         # the timed region's event pairs, created (and their HIP events allocated by one record
         # each) before it starts: one pair per run of steps between resets
         pool[:] = [torch.cuda.Event(enable_timing=True) for _ in range(2 * (K // T + 2))]
@@ -397,6 +435,8 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
+        if spin:
+            torch.cuda._sleep(spin)
         resets = run(W, K, events)
         torch.cuda.synchronize(dev)
         if world > 1:
@@ -508,6 +548,7 @@ def main():
             "store_policy": args.store,
             "alt_store_policy": alt,
             "graph": graph,
+            "launch_pacing": spin_info or None,
         },
         "gather": gather_info,
         "cpu_baseline": cpu,
