@@ -77,6 +77,9 @@ typedef unsigned long long uint64_t;
 #ifndef IMENV_BUF_LOAD
 #define IMENV_BUF_LOAD 0     // 1: exact-row step loads as buffer loads off the block's first env (SGPR bases)
 #endif
+#ifndef IMENV_XCD_REMAP
+#define IMENV_XCD_REMAP 1    // 0: small-block launches keep the identity block -> env chunk map (A/B)
+#endif
 #ifndef IMENV_SLAB_BATCH
 #define IMENV_SLAB_BATCH 1   // 1: a whole group's observation slab is written out in batches of LDS reads
 #endif
@@ -587,6 +590,7 @@ struct DynSpec {
   static constexpr int OBS_ROW = 0;                  // general observation rows are stored directly
   static constexpr bool OBS_STAGE64 = false;         // float64 observations are stored directly
   static constexpr int TD_PRE = 0;                   // in-transit obs slots are loaded after the step
+  static constexpr bool XCD_REMAP = false;           // (step_body)
   using ST = ST_;
   const SpecDev* __restrict__ sp;
   const StepArgs& A;
@@ -1534,7 +1538,16 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   constexpr int SROW = stage_row<P>();   // LDS floats per env (0: observations stored directly)
   const int tid = threadIdx.x;
   const int64_t n = A.n;
-  const int64_t eb = (int64_t)blockIdx.x * EPT * BS;
+  // XCD-aware env chunks (small-block launches): blocks go round-robin to the 8 XCDs (block b to XCD
+  // b mod 8), each with its own L2. A 64-env block's 1-byte ring rows are half a 128-byte line, so two
+  // neighbouring chunks on different XCDs both fetch the line. Chunk c = (b mod 8) * G/8 + b / 8 puts
+  // chunks c and c + 1 on one XCD (a bijection when 8 divides the grid G; otherwise the identity).
+  int64_t bid = blockIdx.x;
+  if constexpr (P::XCD_REMAP && IMENV_XCD_REMAP) {
+    const int64_t G = gridDim.x;
+    if ((G & 7) == 0) bid = (bid & 7) * (G >> 3) + (bid >> 3);
+  }
+  const int64_t eb = bid * EPT * BS;
   const bool poisson = p.demand_layout() == IMENV_LAYOUT_DRAW && p.demand_dist() == IMENV_DEMAND_POISSON;
   // diagnostic phase stamps (IMENV_STAMPS builds, 10 ns ticks of s_memrealtime): 0 entry, 1 loads issued,
   // 2 loads landed (an added vmcnt(0) wait), 3 computed, 4 after the slab barrier, 5 stores issued,
