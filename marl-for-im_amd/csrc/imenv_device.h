@@ -78,7 +78,7 @@ typedef unsigned long long uint64_t;
 #define IMENV_BUF_LOAD 0     // 1: exact-row step loads as buffer loads off the block's first env (SGPR bases)
 #endif
 #ifndef IMENV_XCD_REMAP
-#define IMENV_XCD_REMAP 1    // 0: small-block launches keep the identity block -> env chunk map (A/B)
+#define IMENV_XCD_REMAP 0    // 1: XCD-aware env chunks for small-block launches (measured slower: step_body)
 #endif
 #ifndef IMENV_SLAB_BATCH
 #define IMENV_SLAB_BATCH 1   // 1: a whole group's observation slab is written out in batches of LDS reads
@@ -1538,10 +1538,12 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   constexpr int SROW = stage_row<P>();   // LDS floats per env (0: observations stored directly)
   const int tid = threadIdx.x;
   const int64_t n = A.n;
-  // XCD-aware env chunks (small-block launches): blocks go round-robin to the 8 XCDs (block b to XCD
-  // b mod 8), each with its own L2. A 64-env block's 1-byte ring rows are half a 128-byte line, so two
-  // neighbouring chunks on different XCDs both fetch the line. Chunk c = (b mod 8) * G/8 + b / 8 puts
-  // chunks c and c + 1 on one XCD (a bijection when 8 divides the grid G; otherwise the identity).
+  // XCD-aware env chunks (IMENV_XCD_REMAP=1, small-block launches): blocks go round-robin to the 8
+  // XCDs (block b to XCD b mod 8), each with its own L2. A 64-env block's 1-byte ring rows are half a
+  // 128-byte line, so two neighbouring chunks on different XCDs both fetch the line. Chunk
+  // c = (b mod 8) * G/8 + b / 8 puts chunks c and c + 1 on one XCD (a bijection when 8 divides the
+  // grid G). It removes those fetches (C4: 6.54 -> 5.90 MB read per launch) but the launch gets slower
+  // (5.64 -> 6.04 us, C2 at 131,072 4.20 -> 4.52 us; profiles/r03/xcd_remap/): off by default.
   int64_t bid = blockIdx.x;
   if constexpr (P::XCD_REMAP && IMENV_XCD_REMAP) {
     const int64_t G = gridDim.x;
