@@ -7,7 +7,8 @@ observation-flag combinations the reference's scripts use), not only the bench w
 
 Per config: float32 actions, float32 observations (--obs-f64: float64), in-kernel Philox demand (and noisy delay where the case
 has it), 2 warmup + 2 timed episodes; the step kernel is timed with HIP events on its stream over
-launches t = 1..T-1 of each timed episode. achieved = VectorInvEnv.step_traffic() bytes x n / time.
+launches t = 1..T-1 of each timed episode, queued behind a GPU busy-wait so that small launches are
+timed back to back rather than at the host's pace (round 3). achieved = VectorInvEnv.step_traffic() bytes x n / time.
 One JSON line per config.
 """
 import argparse
@@ -26,6 +27,21 @@ import torch  # noqa: E402
 from golden_io import case_names, fuzz_case_names, load_case  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0
+
+
+_CYCLES_PER_US = {}
+
+
+def spin_cycles(dev, us):
+    """torch.cuda._sleep cycles for about `us` microseconds (calibrated once per device with events)."""
+    if dev not in _CYCLES_PER_US:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        torch.cuda._sleep(200000)
+        e1.record()
+        e1.synchronize()
+        _CYCLES_PER_US[dev] = 200000 / (e0.elapsed_time(e1) * 1e3)
+    return int(us * _CYCLES_PER_US[dev])
 
 
 def run_case(name, n, dev, obs_dtype=torch.float32, store="default"):
@@ -47,6 +63,10 @@ def run_case(name, n, dev, obs_dtype=torch.float32, store="default"):
         e0 = e1 = None
         for t in range(T):
             if t == 1 and ep >= 2:
+                # a GPU busy-wait longer than the host's enqueue of the episode's remaining steps: the
+                # timed launches queue up behind it and run back to back (eager step() costs ~6-8 us of
+                # host time, more than a small launch's kernel)
+                torch.cuda._sleep(spin_cycles(dev, (T - 1) * 20.0))
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
             env.step(acts[t], obs_out=obs, reward_out=rew)
