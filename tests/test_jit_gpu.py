@@ -208,3 +208,42 @@ def test_default_store_policy_by_batch_size(cfg, n, flags):
     got = int(re.search(r"flags=0x([0-9a-f]+)", env.kernel_info()).group(1), 16)
     assert got & 0x6800 == flags, env.kernel_info()
     env.close()
+
+
+@pytest.mark.parametrize("config,n", [("C4", 131072), ("C2", 131072), ("C2", 262144)])
+def test_gpu_launch_size_block_choice_is_invisible(config, n, monkeypatch):
+    """Launches of at most two waves per SIMD (n <= 131,072) take 64-env blocks (JitFlags::small_blocks),
+    larger ones 256; IMENV_JIT_BS forces either. One whole episode (in-kernel Philox demand, write-through
+    stores) under each block size gives the same observations, rewards and state bit for bit."""
+    import bench
+    from imenv import VectorInvEnv
+    kind, cfg = bench.CONFIGS[config][:2]
+    runs = []
+    for bs in (None, "64", "256"):
+        if bs is None:
+            monkeypatch.delenv("IMENV_JIT_BS", raising=False)
+        else:
+            monkeypatch.setenv("IMENV_JIT_BS", bs)
+        monkeypatch.setenv("IMENV_JIT_STRICT", "1")
+        env = VectorInvEnv(kind, cfg, n_envs=n, device=DEV)
+        g = torch.Generator(device=DEV)
+        g.manual_seed(7)
+        T, N = env.T, env.N
+        acts = torch.rand((T, n, N), generator=g, device=DEV) * 2 - 1
+        obs = [env.reset().clone()]
+        rews = []
+        for t in range(T):
+            o, r, _, _ = env.step(acts[t])
+            obs.append(o.clone())
+            rews.append(r.clone())
+        info = env.kernel_info()
+        s = env.state()
+        st = [s["inv"].clone(), s["backlog"].clone(), s["order_u"].clone()]
+        runs.append((int(re.search(r"bs=(\d+)", info).group(1)), torch.stack(obs), torch.stack(rews), st))
+        env.close()
+    assert runs[0][0] == (64 if n <= 131072 else 256), runs[0][0]
+    assert (runs[1][0], runs[2][0]) == (64, 256)
+    for bs, o, r, st in runs[1:]:
+        assert torch.equal(o, runs[0][1]) and torch.equal(r, runs[0][2]), bs
+        for a, b in zip(st, runs[0][3]):
+            assert torch.equal(a, b), bs
