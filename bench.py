@@ -387,6 +387,8 @@ def main():
         ahead (the metric's 2^20-env launches), no spin. Calibrated on two untimed episodes (the step
         sequence stays aligned: 2T steps bring the handle back to the same period). Returns (cycles,
         host us per step, GPU us per step)."""
+        if not hasattr(torch.cuda, "_sleep"):    # (a private torch helper: without it, no pacing)
+            return 0, float("nan"), float("nan")
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize(dev)
         e0.record(stream)
@@ -421,7 +423,8 @@ def main():
         if gather is None:
             spin, h_us, g_us = lead_spin(W, K)
             if not spin_info:      # the line's own timed region (not the informational alt-store run)
-                spin_info.update(host_us_per_step=round(h_us, 3), gpu_us_per_step_queued=round(g_us, 3),
+                spin_info.update(host_us_per_step=None if h_us != h_us else round(h_us, 3),
+                                 gpu_us_per_step_queued=None if g_us != g_us else round(g_us, 3),
                                  lead_spin_cycles=spin)
         # the timed region's event pairs, created (and their HIP events allocated by one record
         # each) before it starts: one pair per run of steps between resets
