@@ -823,7 +823,11 @@ __device__ __forceinline__ void step_core(const P& p, const int t, const int (&o
 #pragma unroll
         for (int k = 0; k < MC; ++k) bto[k] = x1[k];   // A and C drain backlog_to in place
       }
-      const bool second = caseA && ok && amt > 0 && dmp > 0;
+      // (after a guard trip in the first loop the reference has raised, "Infinite Loop 1": no state
+      // follows it. The env's error flag is set; the outstanding-order loop still runs, as in the
+      // oracle's non-raising restatement, so a tripped episode's later values are the oracle's too.
+      // The rollout kernels, which report no per-episode errors, relied on that; plan case 400179.)
+      const bool second = caseA && amt > 0 && dmp > 0;
       int out[MC];
 #pragma unroll
       for (int k = 0; k < MC; ++k) out[k] = oc[k];
