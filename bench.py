@@ -399,9 +399,12 @@ def main():
         n_cal = 2 * T
         torch.cuda._sleep(int(3000 / us_per_cycle))       # 3 ms: longer than enqueueing n_cal steps
         e0.record(stream)
-        h0 = time.perf_counter()
-        run(W, n_cal)
-        h = (time.perf_counter() - h0) * 1e6 / n_cal
+        hs = []
+        for k in range(2):          # two episodes, the faster host pace counts (a descheduled host
+            h0 = time.perf_counter()    # thread in one of them must not buy a long spin)
+            run(W + k * T, T)
+            hs.append((time.perf_counter() - h0) * 1e6 / T)
+        h = min(hs)
         e1.record(stream)
         e1.synchronize()
         g = e0.elapsed_time(e1) * 1e3 / n_cal
