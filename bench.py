@@ -2,23 +2,27 @@
 """Throughput bench for the north-star path: env-steps/s of the HIP step kernel.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4] [--n-envs E]
-                    [--gather] [--no-cpu-baseline]
+                    [--scaling strong|weak] [--gather | --no-gather] [--no-cpu-baseline]
 
 Workload (BASELINE.json metric "env-steps/sec (whole node), 4-stage x 2^20 envs"):
 MultiAgentInvManagement, 4 stages, MA_1 flags (hyperparams.py:344; constants
-inv_management.py:35-56), shared reward, 2^20 envs per GPU, 30-period episodes,
+inv_management.py:35-56), shared reward, 2^20 envs (global), 30-period episodes,
 in-kernel Philox Poisson(5) demand, float32 actions pre-generated [30][n][4]
 (torch.Generator seed 0) and float32 observations written into a [30][n][4][3]
 rollout buffer, float64 rewards. A "step" = one step() of every env; the reset kernel
 runs at each episode boundary, and the line's "resets_timed" says how many of them
 fell inside the timed region.
 
-Multi-GPU: one process per GPU, each rank owns 2^20 envs at env_offset rank*2^20 (weak
-scaling, no data-path collective). The ranks come either from an external launcher
-(torchrun sets WORLD_SIZE / RANK / LOCAL_RANK) or, for `--gpus N` with no launcher, from
-this script itself: the parent process starts N rank processes before it (or they) touch
-the GPU, and exits with the first non-zero rank status. `--gather` adds the optional
-per-step RCCL all-gather of obs+reward; its own time is reported apart from the kernel's.
+Multi-GPU: one process per GPU. By default the ranks STRONG-scale the metric's 2^20 envs (BASELINE.json
+configs[4]): rank r of W steps the contiguous global env ids shard_range(2^20, W, r), so
+the 8-GPU line is C5 (8 x 131,072 envs) and --gpus 1 is the single-GPU metric workload; `--scaling
+weak` gives every rank its own 2^20 envs instead. The ranks come either from an external launcher
+(torchrun sets WORLD_SIZE / RANK / LOCAL_RANK) or, for `--gpus N` with no launcher, from this script
+itself: the parent process starts N rank processes before it (or they) touch the GPU, and exits with
+the first non-zero rank status. With N > 1 (or `--gather`) a second, separately timed pass adds C5's
+per-step all-gather of obs+reward (RCCL over xGMI on the GPU node): the line's value and kernel time
+come from the gather-free pass, the pipelined step+gather rate and the collective's own time are
+reported under "gather".
 The reference's own parallelism is one env per RLlib worker process (hyperparams.py:14,
 MA_inv_management.py:172); the rank processes replace those workers.
 
@@ -209,9 +213,32 @@ def ranks_census(dist, dev):
     return out
 
 
+def shard_plan(scaling, config, n_envs, world, rank):
+    """(global env id of this rank's first env, envs on this rank, global envs of the job).
+
+    strong (default): the job steps n_envs global envs (default: the config's BASELINE.json size, 2^20
+    for C2) and rank r owns the contiguous ids shard_range(n_envs, world, r); so with 8
+    ranks the C2 line is BASELINE's C5, 8 x 131,072 envs. weak: every rank owns n_envs envs of its own,
+    at ids [r * n_envs, (r + 1) * n_envs)."""
+    from imenv.shard import shard_range, weak_offset
+    total = int(n_envs or CONFIGS[config][3])
+    if scaling == "strong":
+        off, n = shard_range(total, world, rank)
+        return off, n, total
+    return weak_offset(total, rank), total, total * world
+
+
+def gather_is_on(args, world):
+    """The per-step all-gather leg: explicit --gather / --no-gather, else on whenever there is more than
+    one rank (C5: the obs / reward batch gathered over xGMI)."""
+    return args.gather if args.gather is not None else world > 1
+
+
 def dry_run(args, world, rank):
     """The launcher / rendezvous / census / max-reduction path with no GPU work (CPU tests, gloo): the
-    line carries n_gpus and ranks_seen, value null."""
+    line carries n_gpus, ranks_seen and the shard plan, value null. With the gather leg on, StepGather
+    runs over CPU tensors with gloo for K steps (every rank writes values derived from its global env
+    ids and each step; every gathered step is checked) and gather_report is computed as on the GPU."""
     import torch
     import torch.distributed as dist
     if os.environ.get("IMENV_BENCH_DRY_FAIL_RANK") == str(rank):     # tests: a rank that dies
@@ -219,17 +246,55 @@ def dry_run(args, world, rank):
     if world > 1:
         dist.init_process_group("gloo")
     census = ranks_census(dist, None)
+    off, n, total = shard_plan(args.scaling, args.config, args.n_envs, world, rank)
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    gather_info = None
+    if gather_is_on(args, world) and world > 1:
+        gather_info = dry_gather(args, dist, world, n, off, total)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "env-steps/s", "n_gpus": world,
                           "dry_run": True, "ranks_seen": len({c["rank"] for c in census}), "ranks": census,
                           "max_over_ranks": t.item(), "launcher": os.environ.get("IMENV_BENCH_LAUNCHER", "external"),
+                          "scaling": args.scaling,
+                          "config": {"n_envs_per_gpu": n, "global_envs": total, "env_offset": off},
+                          "gather": gather_info,
                           "cpu_baseline": json.loads(os.environ[CPU_BASELINE_ENV])
                           if CPU_BASELINE_ENV in os.environ else None}), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def dry_gather(args, dist, world, n, off, total):
+    """StepGather's double-buffered pipeline as bench.py drives it (write into obs_out(s) /
+    reward_out(s), start(s), result(s-1)) on CPU tensors with gloo. The dry run's shards must be equal
+    (the all-gather needs one shape on every rank)."""
+    import torch
+    from imenv.shard import StepGather
+    N, F = 4, 3
+    if total % world:
+        raise SystemExit("dry-run gather: %d envs do not split evenly over %d ranks" % (total, world))
+    ids = torch.arange(off, off + n, dtype=torch.float64)
+    g = StepGather(torch.empty((n, N, F), dtype=torch.float32), torch.empty((n,), dtype=torch.float64))
+    allids = torch.arange(total, dtype=torch.float64)
+
+    def check(s):
+        o, r = g.result(s)
+        want_r = allids * 1000 + s
+        if not (torch.equal(r, want_r) and torch.equal(o[:, 0, 0], (allids % 4096 + s).float())):
+            raise SystemExit("dry-run gather: step %d gathered the wrong values" % s)
+
+    steps = args.steps
+    g.keep_works(True)
+    for s in range(steps):
+        g.obs_out(s).fill_(0.0)[:, 0, 0] = (ids % 4096 + s).float()
+        g.reward_out(s).copy_(ids * 1000 + s)
+        g.start(s)
+        if s > 0:
+            check(s - 1)
+    check(steps - 1)
+    return gather_report(g, dist, None, None, steps, world, n)
 
 
 # ----------------------------------------------------------------- main
@@ -241,14 +306,21 @@ def main():
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS),
                     help="C2 (default): the metric's workload; C3 / C4: BASELINE's other single-GPU configs")
     ap.add_argument("--n-envs", type=int, default=None,
-                    help="envs per GPU (default: 2^20 for C2, BASELINE.json's size for C3 / C4)")
+                    help="envs of the whole job under strong scaling, per GPU under weak scaling (default: "
+                         "2^20 for C2, BASELINE.json's size for C3 / C4)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong (default): the ranks split --n-envs global envs; weak: every rank owns --n-envs")
+    ap.add_argument("--weak", dest="scaling", action="store_const", const="weak", help="same as --scaling weak")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
-    ap.add_argument("--gather", action="store_true", help="add the per-step RCCL all-gather of obs+reward")
+    ap.add_argument("--gather", dest="gather", action="store_true", default=None,
+                    help="time the per-step all-gather of obs+reward in a second pass (default: on with >1 rank)")
+    ap.add_argument("--no-gather", dest="gather", action="store_false")
     ap.add_argument("--store", default="default", choices=["default", "stream", "plain", "writethrough"],
                     help="store policy of the step kernel (imenv_set_store_policy)")
     ap.add_argument("--no-alt-store", action="store_true", help="skip the informational run of the other policy")
     ap.add_argument("--no-graph", action="store_true", help="skip the informational HIP-graph episode replay")
+    ap.add_argument("--no-alt-obs", action="store_true", help="skip the informational float64-observation run")
     ap.add_argument("--cpu-only", action="store_true", help=argparse.SUPPRESS)
     # rehearsal of the multi-rank path on a one-GPU box: every rank on device 0, gloo for the
     # barrier / max-reduction (the driver's N-GPU runs use one GPU per rank and RCCL)
@@ -282,14 +354,15 @@ def main():
         else:
             cpu = cpu_baseline(args.cpu_seconds, args.config)          # before the GPU is initialised
 
-    if args.gather and world > 1 and not args.rehearse_one_gpu:
+    gather_on = gather_is_on(args, world) and world > 1
+    if gather_on and not args.rehearse_one_gpu:
         # RCCL records start / end events around every collective on its own stream (Work._get_duration)
         os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")
     import torch
     import torch.distributed as dist
     from imenv import VectorInvEnv
     from imenv import _native as nat
-    from imenv.shard import StepGather, weak_offset
+    from imenv.shard import StepGather
 
     if args.rehearse_one_gpu:
         local = 0
@@ -307,9 +380,9 @@ def main():
         sys.stderr.write("bench.py: %d ranks took part, world size is %d\n" % (ranks_seen, world))
         sys.exit(3)
 
-    kind, ccfg, cdesc, cn = CONFIGS[args.config]
-    n = args.n_envs or cn
-    env = VectorInvEnv(kind, ccfg, n_envs=n, device=dev, env_offset=weak_offset(n, rank))
+    kind, ccfg, cdesc, _ = CONFIGS[args.config]
+    env_off, n, global_envs = shard_plan(args.scaling, args.config, args.n_envs, world, rank)
+    env = VectorInvEnv(kind, ccfg, n_envs=n, device=dev, env_offset=env_off)
     N, F, T = env.N, env.F, env.T
     g = torch.Generator(device=dev)
     g.manual_seed(0)
@@ -317,9 +390,6 @@ def main():
     obs_buf = torch.empty((T, n, N, F), dtype=torch.float32, device=dev)
     obs0 = torch.empty((n, N, F), dtype=torch.float32, device=dev)
     rew_buf = torch.empty((T,) + env.reward_shape(), dtype=torch.float64, device=dev)
-    gather = None
-    if args.gather and world > 1:
-        gather = StepGather(obs_buf[0], rew_buf[0])
 
     lib, h = env.lib, env._h
     stream = torch.cuda.current_stream(dev)
@@ -337,12 +407,18 @@ def main():
     # duration = elapsed / launches of the run, back-to-back dispatch gaps included, the reset kernel
     # outside every pair. Every timed step launch lies in exactly one pair, whatever K and W are. One
     # pair per episode: a pair per step would cost ~7 us of GPU time each and slow the very loop
-    # being measured (tools/launch_probe.py).
-    def run(first, steps, events=None):
-        """Steps first .. first+steps-1 of the bench's step sequence (period t = step mod T). Returns
-        the number of resets it ran."""
+    # being measured (tools/launch_probe.py). The event pairs are only ever used on the gather-free
+    # pass, so no collective wait lies between them.
+    obs64 = {}     # float64 observation buffers of the informational alt_obs_f64 leg (made on demand)
+
+    def run(first, steps, events=None, gather=None, f64=False):
+        """Steps first .. first+steps-1 of the bench's step sequence (period t = step mod T). With a
+        StepGather the env writes into its send buffers and step s's all-gather runs under step s+1;
+        with f64 the observations are float64 (the reference's dtype). Returns the number of resets it
+        ran."""
         pair = None
         resets = 0
+        op, od = (obs64["ptr"], nat.F64) if f64 else (o_ptr, nat.F32)
         for s in range(first, first + steps):
             t = s % T
             if t == 0:
@@ -354,10 +430,10 @@ def main():
             if pair is not None:
                 pair[2].append(t)
             if gather is None:
-                rc = lib.imenv_step(h, a_ptr[t], nat.F32, o_ptr[t], nat.F32, r_ptr[t], None, None, sptr)
+                rc = lib.imenv_step(h, a_ptr[t], nat.F32, op[t], od, r_ptr[t], None, None, sptr)
             else:
                 # the env writes straight into the packed send buffer of step s (double-buffered); the
-                # all-gather of step s runs on RCCL's stream under step s+1
+                # all-gather of step s runs on the collective's stream under step s+1
                 rc = lib.imenv_step(h, a_ptr[t], nat.F32, gather.obs_out(s).data_ptr(), nat.F32,
                                     gather.reward_out(s).data_ptr(), None, None, sptr)
             if rc:
@@ -369,14 +445,15 @@ def main():
             if gather is not None:
                 gather.start(s)
                 if s > first:
-                    gather.result(s - 1)     # the learner's view of step s-1: [world*n, N, F], [world*n]
+                    gather.result(s - 1)     # the learner's view of step s-1: [global n, N, F], [global n]
         if gather is not None and steps:
             gather.result(first + steps - 1)
         return resets
 
     per_t = env.step_traffic_per_period()
+    per_t64 = env.step_traffic_per_period(obs_bytes=8)
 
-    def lead_spin(W, K):
+    def lead_spin(W, K, f64=False):
         """GPU cycles of a busy-wait (torch.cuda._sleep) to enqueue ahead of the timed launches. Small
         launches (C4 at 131,072 envs: ~5.6 us each) are shorter than the host's enqueue of one step
         (~6 us of Python, ctypes and hipModuleLaunchKernel), so the GPU would idle between launches and
@@ -402,7 +479,7 @@ def main():
         hs = []
         for k in range(2):          # two episodes, the faster host pace counts (a descheduled host
             h0 = time.perf_counter()    # thread in one of them must not buy a long spin)
-            run(W + k * T, T)
+            run(W + k * T, T, f64=f64)
             hs.append((time.perf_counter() - h0) * 1e6 / T)
         h = min(hs)
         e1.record(stream)
@@ -414,21 +491,41 @@ def main():
 
     spin_info = {}
 
-    def timed(W, K):
+    def bracket(body):
+        """The driver's timed region: barrier + synchronise, then body(), then synchronise; the wall time
+        is read before the trailing barrier (every rank's own K steps, not the slowest rank's barrier
+        exit), and the max over ranks is taken afterwards."""
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        out = body()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+        return el, out
+
+    def max_over_ranks(*xs):
+        if world == 1:
+            return xs
+        tt = torch.tensor(list(xs), dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return tuple(v.item() for v in tt)
+
+    def timed(W, K, f64=False):
         """W untimed warmup steps (the first one resets), then exactly K timed steps of the same step
-        sequence, so the timed region holds the resets at its episode boundaries. Returns (wall s,
-        kernel ms per launch, algorithmic bytes per timed launch, timed launches, resets timed), max
-        over ranks."""
+        sequence, so the timed region holds the resets at its episode boundaries. No collective. Returns
+        (wall s, kernel ms per launch, algorithmic bytes per timed launch, timed launches, resets timed),
+        max over ranks."""
         if W == 0:
-            run(0, 1)     # no warmup asked for: one step outside the sequence builds the hipRTC kernel
-        run(0, W)
-        spin = 0
-        if gather is None:
-            spin, h_us, g_us = lead_spin(W, K)
-            if not spin_info:      # the line's own timed region (not the informational alt-store run)
-                spin_info.update(host_us_per_step=None if h_us != h_us else round(h_us, 3),
-                                 gpu_us_per_step_queued=None if g_us != g_us else round(g_us, 3),
-                                 lead_spin_cycles=spin)
+            run(0, 1, f64=f64)     # no warmup asked for: one step outside the sequence builds the hipRTC kernel
+        run(0, W, f64=f64)
+        spin, h_us, g_us = lead_spin(W, K, f64)
+        if not spin_info:      # the line's own timed region (not the informational alt-store run)
+            spin_info.update(host_us_per_step=None if h_us != h_us else round(h_us, 3),
+                             gpu_us_per_step_queued=None if g_us != g_us else round(g_us, 3),
+                             lead_spin_cycles=spin)
         # the timed region's event pairs, created (and their HIP events allocated by one record
         # each) before it starts: one pair per run of steps between resets
         pool[:] = [torch.cuda.Event(enable_timing=True) for _ in range(2 * (K // T + 2))]
@@ -436,27 +533,27 @@ def main():
             e.record(stream)
         torch.cuda.synchronize(dev)
         events = []
-        if gather is not None:
-            gather.keep_works(True)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        if spin:
-            torch.cuda._sleep(spin)
-        resets = run(W, K, events)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
+
+        def body():
+            if spin:
+                torch.cuda._sleep(spin)
+            return run(W, K, events, f64=f64)
+        el, resets = bracket(body)
         # per-launch kernel time and the algorithmic bytes of exactly the launches that were timed
+        pt = per_t64 if f64 else per_t
         kern_ms = sum(a.elapsed_time(b) for a, b, _ in events) / sum(len(ts) for _, _, ts in events)
-        bpl = sum(per_t[t] for _, _, ts in events for t in ts) * n / sum(len(ts) for _, _, ts in events)
-        if world > 1:
-            tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            el, kern_ms = tt[0].item(), tt[1].item()
+        bpl = sum(pt[t] for _, _, ts in events for t in ts) * n / sum(len(ts) for _, _, ts in events)
+        el, kern_ms = max_over_ranks(el, kern_ms)
         return el, kern_ms, bpl, sum(len(ts) for _, _, ts in events), resets
+
+    def timed_gather(W, K, gather):
+        """The same W + K step sequence with C5's per-step all-gather pipelined under the next step (a
+        second pass after the line's own): the wall time of the K steps including every collective, max
+        over ranks."""
+        run(0, max(W, 1), gather=gather)
+        gather.keep_works(True)
+        el, _ = bracket(lambda: run(W, K, gather=gather))
+        return max_over_ranks(el)[0]
 
     pool = []
     W, K = args.warmup, args.steps
@@ -465,8 +562,20 @@ def main():
     kinfo = env.kernel_info()          # the timed kernel (before the informational runs below)
 
     gather_info = None
-    if gather is not None:
-        gather_info = gather_report(gather, dist, dev, stream, K, world, n)
+    if gather_on:
+        backend = dist.get_backend()
+        try:
+            gth = StepGather(obs_buf[0], rew_buf[0])
+            g_el = timed_gather(W, K, gth)
+            gather_info = gather_report(gth, dist, dev, stream, K, world, n)
+            gather_info.update(backend="gloo (one-GPU rehearsal)" if args.rehearse_one_gpu else
+                               "%s (RCCL over xGMI)" % backend if backend == "nccl" else backend,
+                               pipelined_value=round(global_envs * K / g_el, 1),
+                               pipelined_ms_per_step=round(g_el / K * 1e3, 6),
+                               pipelined_over_gather_free=round(el / g_el, 4))
+            del gth
+        except Exception as ex:          # informational leg: the line still reports the gather-free pass
+            gather_info = {"error": "%s: %s" % (type(ex).__name__, str(ex)[:300])}
 
     alt = None
     if world == 1 and not args.no_alt_store:
@@ -482,8 +591,22 @@ def main():
                "kernel_us": round(a_kern * 1e3, 3), "achieved": round(a_bpl / (a_kern * 1e-3) / 1e9, 1),
                "frac": round(a_bpl / (a_kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
+    alt64 = None
+    if world == 1 and not args.no_alt_obs:
+        # the reference's observation dtype (float64, IM_env.py:231-285), same store policy, same handle
+        ob64 = torch.empty((T, n, N, F), dtype=torch.float64, device=dev)
+        obs64["ptr"] = [ob64[t].data_ptr() for t in range(T)]
+        f_el, f_kern, f_bpl, _, _ = timed(W, K, f64=True)
+        alt64 = {"kernel": env.kernel_info(), "value": round(n * K / f_el, 1), "ms_per_step": round(f_el / K * 1e3, 6),
+                 "kernel_us": round(f_kern * 1e3, 3), "bytes_per_env_step": round(f_bpl / n, 3),
+                 "achieved": round(f_bpl / (f_kern * 1e-3) / 1e9, 1),
+                 "frac": round(f_bpl / (f_kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                 "traffic": pmc_traffic(n, env.kernel_info())}
+        del ob64
+        obs64.clear()
+
     graph = None
-    if world == 1 and gather is None and not args.no_graph:
+    if world == 1 and not args.no_graph:
         graph = graph_episode_run(torch, env, reset, lib, nat, a_ptr, o_ptr, r_ptr, per_t, n, T, dev)
 
     # measured stream-copy ceiling at the step's byte count: a device copy of half the
@@ -503,12 +626,20 @@ def main():
     copy_gbs = 2 * half * 20 / (c0.elapsed_time(c1) * 1e-3) / 1e9
     del csrc, cdst
 
-    total_env_steps = world * n * K
-    value = total_env_steps / el
+    value = global_envs * K / el
     es = env.state_layout()[0]
+    if kinfo.startswith("jit-diag:"):
+        # IMENV_ABLATE / IMENV_STAMPS builds (IMENV_DIAG=1): wrong results or extra stores by design
+        sys.stderr.write("bench.py: the timed kernel is a diagnostic build (%s): not a bench line\n" % kinfo)
     achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic = pmc_traffic(n, kinfo)
     launcher = os.environ.get("IMENV_BENCH_LAUNCHER", "external" if world > 1 else "none")
+    size = "2^20" if global_envs == 1 << 20 else str(global_envs)
+    if args.scaling == "strong":
+        shards = ("%s envs in all, %d per GPU (rank r steps global env ids shard_range(%d, %d, r))"
+                  % (size, n, global_envs, world)) if world > 1 else "%s envs on one GPU" % size
+    else:
+        shards = "%s envs per GPU, %d in all (weak scaling)" % (str(n), global_envs)
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -518,24 +649,26 @@ def main():
         "warmup": W,
         "ms_per_step": round(el / K * 1e3, 6),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": "%s state, f64 reward, f32 obs/actions" % {1: "u8", 2: "int16", 4: "int32"}[es],
+        "dtype": "%s state (exact: the spec's proven value bounds fit it), f64 reward, f32 obs/actions"
+                 % {1: "u8", 2: "int16", 4: "int32"}[es],
         "data": "synthetic: in-kernel Philox4x32-10 Poisson(5) demand, uniform[-1,1] f32 actions (torch seed 0)",
         "ranks_seen": ranks_seen,
         "gpus_seen": gpus_seen if not args.rehearse_one_gpu else 1,
         "launcher": launcher,
         "resets_timed": resets_timed,
         "config": {
-            "workload": "%s%s: %s, %s envs per GPU, 30-period episodes; %d timed steps, %d of them "
+            "workload": "%s%s: %s, %s, 30-period episodes; %d timed steps, %d of them "
                         "preceded by the episode's reset kernel inside the timed region"
-                        % (args.config, " shape at the metric's size" if args.config == "C2" else "", cdesc,
-                           "2^20" if n == 1 << 20 else str(n), K, resets_timed),
-            "n_envs_per_gpu": n, "global_envs": world * n, "num_stages": N, "obs_features": F,
-            "num_periods": T,
-            "parallelism": "env-sharded x%d (one process per GPU%s, no data-path collective%s)"
+                        % (args.config, " at the metric's size" if args.config == "C2" and global_envs == 1 << 20
+                           else "", cdesc, shards, K, resets_timed),
+            "n_envs_per_gpu": n, "global_envs": global_envs, "env_offset": env_off, "num_stages": N,
+            "obs_features": F, "num_periods": T,
+            "parallelism": "env-sharded x%d (one process per GPU%s, no data-path collective in the timed pass%s)"
                            % (world, ", all on GPU 0 with gloo: rehearsal" if args.rehearse_one_gpu else "",
-                              ", + RCCL all-gather of obs/reward per step" if gather is not None else ""),
+                              "; the per-step all-gather of obs/reward timed in a second pass (\"gather\")"
+                              if gather_on else ""),
         },
         "roofline": {
             "bound": "hbm",
@@ -554,12 +687,16 @@ def main():
             "bytes_per_launch": round(bytes_per_launch),
             "store_policy": args.store,
             "alt_store_policy": alt,
+            "alt_obs_f64": alt64,
             "graph": graph,
             "launch_pacing": spin_info or None,
         },
         "gather": gather_info,
         "cpu_baseline": cpu,
     }
+    if kinfo.startswith("jit-diag:"):
+        out["diagnostic_build"] = True
+        out["roofline"]["traffic"] = None
     if cpu:
         out["cpu_baseline"]["gpu_over_cpu"] = round(value / cpu["value"], 1)
     if rank == 0:
@@ -570,10 +707,11 @@ def main():
 
 
 def gather_report(gather, dist, dev, stream, K, world, n):
-    """The per-step all-gather's own time, apart from the kernel's: (1) RCCL's start / end events on its
-    own stream for each collective of the timed region (Work._get_duration, TORCH_NCCL_ENABLE_TIMING),
-    mean and max over ranks; (2) the same collective timed alone, K back to back, with events on the
-    current stream (which waits on RCCL's stream after each). Bytes are the packed send buffer."""
+    """The per-step all-gather's own time, apart from the kernel's: (1) the collective stream's start /
+    end events for each collective of the pipelined pass (Work._get_duration, TORCH_NCCL_ENABLE_TIMING;
+    RCCL only), mean and max over ranks; (2) the same collective timed alone, K back to back (events on
+    the current stream, which waits on the collective's after each; host clock on CPU tensors). Bytes
+    are the packed send buffer."""
     import torch
     works = gather.keep_works(False)
     in_loop = None
@@ -587,28 +725,35 @@ def gather_report(gather, dist, dev, stream, K, world, n):
     reps = max(5, min(K, 50))
     gather.start(0)
     gather.wait(0)
-    torch.cuda.synchronize(dev)
+    if dev is not None:
+        torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
+    if dev is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+    h0 = time.perf_counter()
     for _ in range(reps):
         gather.start(0)
         gather.wait(0)
-    e1.record(stream)
-    e1.synchronize()
-    alone = e0.elapsed_time(e1) / reps
-    t = torch.tensor([in_loop if in_loop is not None else -1.0, alone], dtype=torch.float64, device=dev)
+    if dev is not None:
+        e1.record(stream)
+        e1.synchronize()
+        alone = e0.elapsed_time(e1) / reps
+    else:
+        alone = (time.perf_counter() - h0) * 1e3 / reps
+    t = torch.tensor([in_loop if in_loop is not None else -1.0, alone], dtype=torch.float64,
+                     device=dev if dev is not None else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     in_loop_max = t[0].item() if in_loop is not None else None
     recv = gather.chunk * world
     return {
-        "collective": "all_gather_into_tensor" if gather._into else "all_gather (gloo)",
+        "collective": "all_gather_into_tensor" if gather._into else "all_gather (list form)",
         "send_bytes_per_rank": gather.chunk, "recv_bytes_per_rank": recv,
         "gather_us": round(in_loop_max * 1e3, 3) if in_loop_max is not None else None,
-        "gather_us_source": "RCCL stream events per timed collective (max over ranks of the mean)"
-                            if in_loop_max is not None else "unavailable",
+        "gather_us_source": "collective-stream events per pipelined collective (max over ranks of the mean)"
+                            if in_loop_max is not None else "unavailable (backend records no per-collective times)",
         "gather_alone_us": round(t[1].item() * 1e3, 3),
         "gather_alone_recv_gbs": round(recv / (t[1].item() * 1e-3) / 1e9, 1),
         "collectives_timed": len(works),

@@ -366,21 +366,16 @@ int fail(int code, const std::string& msg) {
     if (_e != hipSuccess) return fail(IMENV_E_HIP, std::string(#x ": ") + hipGetErrorString(_e));    \
   } while (0)
 
-// Integer tuning switch from the environment, read once per process per name (a cached policy, not a
-// getenv per call). Unset or unparsable: dflt.
+// Integer tuning switch from the environment, read on every call (a getenv is cheap next to a kernel
+// launch, and a test that changes the variable between calls sees its new value). Unset or
+// unparsable: dflt.
 int env_switch(const char* name, int dflt) {
-  static std::mutex mu;
-  static std::unordered_map<std::string, int> cache;
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find(name);
-  if (it != cache.end()) return it->second;
   int v = dflt;
   if (const char* e = std::getenv(name)) {
     char* end = nullptr;
     const long x = std::strtol(e, &end, 10);
     if (end && end != e) v = (int)x;
   }
-  cache.emplace(name, v);
   return v;
 }
 
@@ -578,7 +573,10 @@ int validate_and_derive(const ImEnvSpec& s, SpecDev& d, int& maxc) {
         !std::isfinite(s.backlog_cost[i]) || !std::isfinite(s.inv_target[i]))
       return fail(IMENV_E_INVALID, "prices, costs and inventory targets must be finite");
     for (int q = 0; q < 4; ++q)
-      if (s.split_limit[i][q] < 0) return fail(IMENV_E_INVALID, "split guard limits must be >= 0");
+      // the closed-form round robin (rr_closed) counts rounds up to limit + 1 in int32; the reference's
+      // guards are a few multiples of a node's demand bound, far below 2^30
+      if (s.split_limit[i][q] < 0 || s.split_limit[i][q] > (1 << 30))
+        return fail(IMENV_E_INVALID, "split guard limits must be in [0, 2^30]");
   }
   for (int g = 0; g < IMENV_NUM_GROUPS; ++g) {
     if (s.group_mode[g] != IMENV_OBS_SCALED && s.group_mode[g] != IMENV_OBS_CLAMP_SCALED) continue;

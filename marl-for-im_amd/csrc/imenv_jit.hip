@@ -143,6 +143,40 @@ std::string flit(float x) {
 // values outside it take the reference expression (an IEEE double division: exact for every value).
 constexpr int64_t kVerifyMax = 1 << 16;
 
+// The largest raw value an observation of group g at node i can read, restated from the state bounds
+// (imenv_capi.hip: demand_bound / state_bound): inventory and order_u are clipped to inv_max
+// (IM_env.py:328-340); backlog to its cap, else T periods of demand; demand history to the node's
+// demand bound; order history to order_max; an in-transit slot holds one shipment (backlog + demand +
+// the split's overshoot, or the factory's order); node ids to N. emit_obs_hooks emits an unguarded
+// closed form only when this bound lies inside the verified range [0, vbound] (a cross-check of
+// state_bound: a feature that read a value beyond it would keep the guarded form, exact everywhere).
+int64_t obs_source_bound(const ImEnvSpec& s, int g, int i) {
+  auto dbound = [&](int k) -> int64_t {
+    if (s.retailer_slot[k] >= 0) return s.inv_max[k];
+    int64_t b = 0;
+    for (int c = 0; c < s.num_nodes; ++c)
+      if (s.demand_parent[c] == k) b += s.order_max[c];
+    return b;
+  };
+  auto blbound = [&](int k) -> int64_t {
+    return s.backlog_cap[k] >= 0 ? (int64_t)s.backlog_cap[k] : (int64_t)s.num_periods * dbound(k);
+  };
+  switch (g) {
+    case IMENV_G_INV: return std::max<int64_t>(s.inv_max[i], s.init_inv[i]);
+    case IMENV_G_ORDER_U: return s.inv_max[i];
+    case IMENV_G_BACKLOG: return blbound(i);
+    case IMENV_G_DEMAND_HIST: return dbound(i);
+    case IMENV_G_ORDER_HIST: return s.order_max[i];
+    case IMENV_G_TRANSIT: {
+      const int par = s.parent[i];
+      if (par < 0) return s.order_max[i];
+      return blbound(par) + dbound(par) + IMENV_MAX_CHILDREN;
+    }
+    case IMENV_G_NODE_ID: return s.num_nodes;
+    default: return INT64_MAX;
+  }
+}
+
 void emit_obs_hooks(std::ostream& o, const SpecDev& d) {
   const ImEnvSpec& s = d.s;
   const bool use = !(std::getenv("IMENV_JIT_OBS") && std::string(std::getenv("IMENV_JIT_OBS")) == "lut");
@@ -160,9 +194,9 @@ void emit_obs_hooks(std::ostream& o, const SpecDev& d) {
       const bool clamp = mode == IMENV_OBS_CLAMP_SCALED;
       const bool int_clip = clamp && clip >= 0.0 && clip == std::floor(clip) && clip < (double)kVerifyMax;
       int64_t hi = d.vbound;
-      bool full = hi <= kVerifyMax;
+      bool full = hi <= kVerifyMax && obs_source_bound(s, g, i) <= (int64_t)d.vbound;
       if (clamp) {
-        if (int_clip) { hi = std::min<int64_t>(hi, (int64_t)clip); full = true; }
+        if (int_clip) { hi = (int64_t)clip; full = true; }   // every value is clamped to clip first
         else full = false;
       }
       if (!full) hi = mx;
@@ -382,10 +416,54 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
 }
 }  // namespace
 
-// the streaming- and write-through-store variants have names of their own, so kernel traces and PMC
-// summaries never average them with the plain-store kernel
-static const char* jit_kernel_name(const JitFlags& f) {
-  return f.stream_store ? "imenv_step_jit_nt" : (f.wt_obs || f.wt_state) ? "imenv_step_jit_wt" : "imenv_step_jit";
+namespace {
+// Extra hipRTC options (IMENV_JIT_OPTS, tuning experiments such as -DIMENV_BUF_LOAD=1) change the kernel
+// without changing the spec or the flags, so a hash of them goes into the kernel's name and its tag:
+// a kernel trace or a PMC summary of an experiment never matches the production kernel's. Diagnostic
+// switches (IMENV_ABLATE gives WRONG results on purpose; IMENV_STAMPS writes phase stamps) are refused
+// unless IMENV_DIAG=1 is set too, and their tag starts "jit-diag:" (bench.py and tools/pmc_summary.py
+// reject such kernels).
+std::string jit_extra_opts() {
+  const char* v = std::getenv("IMENV_JIT_OPTS");
+  return v ? std::string(v) : std::string();
+}
+uint32_t fnv1a(const std::string& x) {
+  uint32_t h = 2166136261u;
+  for (char c : x) h = (h ^ (uint8_t)c) * 16777619u;
+  return h;
+}
+bool diag_opts(const std::string& x) {
+  return x.find("IMENV_ABLATE") != std::string::npos || x.find("IMENV_STAMPS") != std::string::npos;
+}
+// "", or "_opt_<hash>" / "_diag_<hash>" for a kernel built with extra options
+std::string opts_suffix() {
+  const std::string x = jit_extra_opts();
+  if (x.find_first_not_of(" \t") == std::string::npos) return "";
+  char b[32];
+  std::snprintf(b, sizeof b, "_%s_%08x", diag_opts(x) ? "diag" : "opt", fnv1a(x));
+  return b;
+}
+}  // namespace
+
+// the streaming- and write-through-store variants, and float64-observation kernels, have names of their
+// own, so kernel traces and PMC summaries never average them with another variant
+static std::string jit_kernel_name(const JitFlags& f) {
+  return std::string(f.stream_store ? "imenv_step_jit_nt" : (f.wt_obs || f.wt_state) ? "imenv_step_jit_wt"
+                                                                                     : "imenv_step_jit") +
+         (f.obs_f64 ? "_o64" : "") + opts_suffix();
+}
+
+// the tag's prefix: "jit:", or "jit-diag:" for a diagnostic build
+static const char* tag_prefix() { return diag_opts(jit_extra_opts()) ? "jit-diag:" : "jit:"; }
+
+// a diagnostic build needs IMENV_DIAG=1 (never taken by accident from a stray IMENV_JIT_OPTS)
+static bool diag_refused(std::string& msg) {
+  const std::string x = jit_extra_opts();
+  if (!diag_opts(x)) return false;
+  const char* d = std::getenv("IMENV_DIAG");
+  if (d && std::atoi(d) != 0) return false;
+  msg = "IMENV_JIT_OPTS='" + x + "' builds a diagnostic kernel (IMENV_ABLATE / IMENV_STAMPS); set IMENV_DIAG=1 to allow it";
+  return true;
 }
 
 std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f) {
@@ -502,14 +580,17 @@ bool load_module(const std::string& src, const std::string& arch, const char* fn
 
 bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const std::string& arch, JitKernel& out,
               std::string& msg) {
+  if (diag_refused(msg)) return false;
   const std::string src = jit_source(d, maxc, base, f);
-  if (!load_module(src, arch, jit_kernel_name(f), out, msg)) return false;
+  if (!load_module(src, arch, jit_kernel_name(f).c_str(), out, msg)) return false;
   out.ept = jit_envs_per_thread(d, base, f.obs_f64);
   out.bs = jit_step_block_size(d, base, f.obs_f64 ? 8 : 4, out.ept, f.small_blocks);
-  char tag[160];
-  // dev=: hash of the device-code header, so a profile of an older kernel body never matches this one
-  std::snprintf(tag, sizeof tag, "jit:%s[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,ept=%d,%zuB,dev=%08x]",
-                jit_kernel_name(f), d.s.num_nodes, maxc, base ? 1 : 0, d.es, f.key(), out.bs, out.ept, src.size(), device_src_hash());
+  char tag[224];
+  // dev=: hash of the device-code header, so a profile of an older kernel body never matches this one;
+  // the kernel name carries the hash of any extra compile options
+  std::snprintf(tag, sizeof tag, "%s%s[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,ept=%d,%zuB,dev=%08x]", tag_prefix(),
+                jit_kernel_name(f).c_str(), d.s.num_nodes, maxc, base ? 1 : 0, d.es, f.key(), out.bs, out.ept,
+                src.size(), device_src_hash());
   out.tag = tag;
   return true;
 }
@@ -554,7 +635,7 @@ std::string jit_rollout_source(const SpecDev& d, int maxc, const RolloutFlags& f
   const int pmf = f.objective ? kRolloutPmfLds : 1;
   const int tb = rollout_term_slots(d, f);
   o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
-       "imenv_rollout_jit(const imenv::SpecDev* __restrict__ sp, const imenv::RolloutArgs A) {\n"
+    << "imenv_rollout_jit" << opts_suffix() << "(const imenv::SpecDev* __restrict__ sp, const imenv::RolloutArgs A) {\n"
        "  __shared__ uint32_t s_thr["
     << (d.s.demand_dist == IMENV_DEMAND_POISSON && !f.table ? IMENV_TABLE_MAX : 1)
     << "];\n"
@@ -581,12 +662,15 @@ bool jit_rollout_load(const SpecDev& d, int maxc, const RolloutFlags& f, const s
     msg = "rollout: the in-transit queue exceeds 64 KiB of LDS at 64 threads per block";
     return false;
   }
+  if (diag_refused(msg)) return false;
   const std::string src = jit_rollout_source(d, maxc, f, bs);
-  if (!load_module(src, arch, "imenv_rollout_jit", out, msg)) return false;
+  const std::string name = "imenv_rollout_jit" + opts_suffix();
+  if (!load_module(src, arch, name.c_str(), out, msg)) return false;
   out.bs = bs;
-  char tag[160];
-  std::snprintf(tag, sizeof tag, "jit:imenv_rollout_jit[N=%d,MC=%d,es=%d,flags=0x%x,bs=%d,tb=%d,%zuB,dev=%08x]",
-                d.s.num_nodes, maxc, d.es, f.key(), bs, rollout_term_slots(d, f), src.size(), device_src_hash());
+  char tag[224];
+  std::snprintf(tag, sizeof tag, "%s%s[N=%d,MC=%d,es=%d,flags=0x%x,bs=%d,tb=%d,%zuB,dev=%08x]", tag_prefix(),
+                name.c_str(), d.s.num_nodes, maxc, d.es, f.key(), bs, rollout_term_slots(d, f), src.size(),
+                device_src_hash());
   out.tag = tag;
   return true;
 }

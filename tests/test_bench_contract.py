@@ -41,7 +41,8 @@ def test_bench_json_line(steps, warmup):
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in d, k
-    assert d["n_gpus"] == 1 and d["steps"] == steps and d["warmup"] == warmup and d["scaling"] == "weak" and d["higher_is_better"] is True
+    assert d["n_gpus"] == 1 and d["steps"] == steps and d["warmup"] == warmup and d["scaling"] == "strong"
+    assert d["higher_is_better"] is True and d["config"]["global_envs"] == 1 << 20
     assert d["value"] > 0 and d["ms_per_step"] > 0
     assert d["config"]["n_envs_per_gpu"] == 1 << 20 and "workload" in d["config"]
     r = d["roofline"]
@@ -82,7 +83,7 @@ def test_gpus_n_spawns_n_ranks_itself():
     127.0.0.1, census of ranks, max-reduction), hands them the CPU baseline it measured first, and
     rank 0 prints one line with n_gpus 2 and ranks_seen 2 (the reference's own parallelism: one env
     per RLlib worker process, hyperparams.py:14)."""
-    r = _run_rc(["--gpus", "2", "--dry-run", "--cpu-seconds", "0.2"], timeout=300)
+    r = _run_rc(["--gpus", "2", "--dry-run", "--no-gather", "--cpu-seconds", "0.2"], timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout           # rank 0 only
@@ -90,6 +91,58 @@ def test_gpus_n_spawns_n_ranks_itself():
     assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["launcher"] == "self"
     assert sorted(x["rank"] for x in d["ranks"]) == [0, 1] and d["max_over_ranks"] == 2.0
     assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["kind"] == "port"
+    # strong scaling by default: the metric's 2^20 envs split over the ranks (C5 at 8 ranks)
+    assert d["scaling"] == "strong" and d["config"]["global_envs"] == 1 << 20
+    assert d["config"]["n_envs_per_gpu"] == 1 << 19 and d["gather"] is None
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 5, 6, 7, 8])
+def test_strong_shard_plan_covers_the_metric_size(world):
+    """Every N: the ranks' contiguous shards cover global env ids [0, 2^20) exactly once (SURVEY.md §8e:
+    rank r owns [r*n/W, (r+1)*n/W)), so the N-GPU line always steps the metric's 2^20 envs; at N = 8
+    each rank steps 131,072 envs (BASELINE.json configs[4], C5)."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "marl-for-im_amd"))
+    import bench
+    plans = [bench.shard_plan("strong", "C2", None, world, r) for r in range(world)]
+    assert all(total == 1 << 20 for _, _, total in plans)
+    assert plans[0][0] == 0 and sum(n for _, n, _ in plans) == 1 << 20
+    for (o0, n0, _), (o1, _, _) in zip(plans, plans[1:]):
+        assert o1 == o0 + n0
+    assert max(n for _, n, _ in plans) - min(n for _, n, _ in plans) <= 1
+    if world == 8:
+        assert {n for _, n, _ in plans} == {131072}
+    # weak scaling: every rank its own 2^20 envs, at ids r * 2^20
+    weak = [bench.shard_plan("weak", "C2", None, world, r) for r in range(world)]
+    assert [o for o, _, _ in weak] == [r << 20 for r in range(world)]
+    assert all(n == 1 << 20 and total == world << 20 for _, n, total in weak)
+
+
+def test_gather_leg_runs_step_gather_over_gloo():
+    """`--gpus 2 --dry-run --gather`: both ranks drive StepGather's double-buffered pipeline (write into
+    obs_out(s) / reward_out(s), start(s), result(s-1)) on CPU tensors with gloo, every gathered step is
+    checked against the global env ids, and gather_report fills the line's "gather" object."""
+    steps = 7
+    r = _run_rc(["--gpus", "2", "--dry-run", "--gather", "--no-cpu-baseline", "--n-envs", "4096",
+                 "--steps", str(steps)], timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    g = d["gather"]
+    assert d["config"]["global_envs"] == 4096 and d["config"]["n_envs_per_gpu"] == 2048
+    assert g["collectives_timed"] == steps and g["gather_alone_us"] > 0
+    # packed send buffer: obs [2048, 4, 3] f32 + reward [2048] f64, each field 256-byte aligned
+    assert g["send_bytes_per_rank"] == 2048 * 12 * 4 + 2048 * 8 and g["recv_bytes_per_rank"] == 2 * g["send_bytes_per_rank"]
+    # on by default with more than one rank
+    r = _run_rc(["--gpus", "2", "--dry-run", "--no-cpu-baseline", "--n-envs", "4096", "--steps", "3"], timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])["gather"]["collectives_timed"] == 3
+
+
+def test_weak_scaling_flag():
+    r = _run_rc(["--gpus", "2", "--dry-run", "--no-gather", "--no-cpu-baseline", "--weak"], timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["scaling"] == "weak" and d["config"]["global_envs"] == 2 << 20 and d["config"]["n_envs_per_gpu"] == 1 << 20
 
 
 def test_gpus_disagreeing_with_launcher_world_fails():

@@ -86,6 +86,37 @@ def test_gpu_jit_failure_falls_back_for_its_flag_set_only(monkeypatch):
     env.close()
 
 
+def test_gpu_diagnostic_builds_need_imenv_diag(monkeypatch):
+    """A diagnostic compile switch in IMENV_JIT_OPTS (IMENV_ABLATE: wrong results by design) is refused
+    at kernel load without IMENV_DIAG=1: the flag set runs on the ahead-of-time kernel, bit-exact, and
+    kernel_info says why. With IMENV_DIAG=1 a diagnostic build (here IMENV_STAMPS, which leaves the
+    results alone when no stamp buffer is attached) loads, and its tag starts "jit-diag:" with a kernel
+    name of its own, so bench.py and tools/pmc_summary.py can refuse it."""
+    from imenv import VectorInvEnv
+    monkeypatch.setenv("IMENV_JIT_STRICT", "0")
+    monkeypatch.delenv("IMENV_DIAG", raising=False)
+    meta, d = load_case("C2_MAIM4")
+    monkeypatch.setenv("IMENV_JIT_OPTS", "-DIMENV_ABLATE=16")
+    env = VectorInvEnv(meta["kind"], meta["config"], n_envs=meta["E"], device=DEV, obs_dtype=torch.float32)
+    _episode(env, meta, d, torch.float32)
+    info = env.kernel_info()
+    assert info.startswith("aot:") and "IMENV_DIAG" in info, info
+    env.close()
+    monkeypatch.setenv("IMENV_JIT_OPTS", "-DIMENV_STAMPS=1")
+    monkeypatch.setenv("IMENV_DIAG", "1")
+    env = VectorInvEnv(meta["kind"], meta["config"], n_envs=meta["E"], device=DEV, obs_dtype=torch.float32)
+    _episode(env, meta, d, torch.float32)
+    info = env.kernel_info()
+    assert re.match(r"jit-diag:imenv_step_jit_wt_diag_[0-9a-f]{8}\[", info), info
+    env.close()
+    monkeypatch.setenv("IMENV_JIT_OPTS", "-DIMENV_SLAB_BATCH=1")     # a tuning option: not diagnostic
+    monkeypatch.delenv("IMENV_DIAG")
+    env = VectorInvEnv(meta["kind"], meta["config"], n_envs=meta["E"], device=DEV, obs_dtype=torch.float32)
+    _episode(env, meta, d, torch.float32)
+    assert re.match(r"jit:imenv_step_jit_wt_opt_[0-9a-f]{8}\[", env.kernel_info()), env.kernel_info()
+    env.close()
+
+
 @pytest.mark.parametrize("name", ["C2_MAIM4", "C3_IM8", "MAIM_div2_share"])
 @pytest.mark.parametrize("odt", ["f32", "f64"])
 @pytest.mark.parametrize("mode", [1, 0])

@@ -127,3 +127,49 @@ def test_library_embeds_the_current_device_sources():
         text = open(path, "rb").read()
         assert blob.find(text + b"\0") >= 0, \
             "%s differs from the copy embedded in libimenv.so: rebuild (python __graft_entry__.py build)" % path
+
+
+def _dump_jit_source(cname, tmp_path, extra_env=None):
+    """The generated hipRTC source of a bench config's step kernel (f32 actions / obs, write-through
+    stores), from a fresh process (IMENV_JIT_DUMP; the compile cache is per process)."""
+    import subprocess
+    import sys
+    code = ("import ctypes, bench; from imenv import _native, build_spec; lib = _native.load(); "
+            "k, c = bench.CONFIGS[%r][:2]; s = build_spec(k, c).to_c(); log = ctypes.create_string_buffer(65536); "
+            "rc = lib.imenv_jit_check(ctypes.byref(s), b'gfx950', 0x2000, log, len(log)); "
+            "assert rc == 0, log.value.decode()[:2000]" % cname)
+    os.makedirs(tmp_path, exist_ok=True)
+    env = dict(os.environ, IMENV_JIT_DUMP=str(tmp_path), **(extra_env or {}))
+    env["PYTHONPATH"] = os.pathsep.join([ROOT, os.path.join(ROOT, "marl-for-im_amd")])
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    srcs = [p for p in os.listdir(tmp_path) if p.endswith(".hip")]
+    assert len(srcs) == 1, srcs
+    return open(os.path.join(tmp_path, srcs[0])).read()
+
+
+@pytest.mark.parametrize("cname", ["C2", "C3", "C4"])
+def test_bench_kernels_use_unguarded_verified_observations(cname, tmp_path):
+    """Every scaled observation value of the bench configs is emitted as a closed form verified
+    exhaustively over [0, vbound] with no per-value range guard: the values an observation reads
+    (obs_source_bound: capacities, capped backlog, demand and shipment bounds) all lie inside the
+    verified range (imenv_jit.hip emit_obs_hooks keeps the guard otherwise)."""
+    from imenv import _native
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libimenv.so not built")
+    src = _dump_jit_source(cname, tmp_path)
+    assert "if ((unsigned)v <=" not in src
+    assert "imenv_step_jit_wt(" in src
+
+
+def test_extra_jit_options_rename_the_kernel(tmp_path):
+    """IMENV_JIT_OPTS experiments get a kernel name of their own (a hash of the options), so a trace or
+    PMC summary of an experiment never matches the production kernel; diagnostic switches are named
+    _diag_ (and refused at kernel load unless IMENV_DIAG=1: tests/test_jit_gpu.py)."""
+    from imenv import _native
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libimenv.so not built")
+    src = _dump_jit_source("C2", tmp_path / "opt", {"IMENV_JIT_OPTS": "-DIMENV_SLAB_BATCH=1"})
+    assert re.search(r"imenv_step_jit_wt_opt_[0-9a-f]{8}\(", src)
+    src = _dump_jit_source("C2", tmp_path / "diag", {"IMENV_JIT_OPTS": "-DIMENV_ABLATE=16"})
+    assert re.search(r"imenv_step_jit_wt_diag_[0-9a-f]{8}\(", src)

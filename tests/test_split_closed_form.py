@@ -15,3 +15,13 @@ def test_two_child_round_robin_closed_form_equals_literal_loop():
     assert n > 50000
     assert not bad, bad[:5]
 
+
+
+def test_closed_form_at_the_largest_accepted_guard_limit():
+    """imenv_create accepts split guard limits up to 2^30 (tools/asan_host_check.py: 2^30 + 1 and
+    INT32_MAX are refused): at 2^30 the int32 closed form still equals the literal loop, while at
+    INT32_MAX its `lim + 1` would wrap (the reason for the bound)."""
+    n, bad = check(xr=range(-2, 9), ar=range(-2, 20), lims=(1 << 30,))
+    assert n > 4000 and not bad, bad[:5]
+    _, bad = check(xr=range(1, 4), ar=range(1, 6), lims=(2 ** 31 - 1,))
+    assert bad      # documents the overflow that validation prevents

@@ -155,6 +155,9 @@ def malformed(base):
         mut("group_den_nan", lambda s: s.group_den[0].__setitem__(0, nan)),
         mut("group_clip_neg_inf", lambda s: (s.group_mode.__setitem__(5, 3), s.group_clip[5].__setitem__(0, -inf))),
         mut("split_limit_neg", lambda s: s.split_limit[0].__setitem__(0, -1)),
+        # the closed-form split counts rounds up to limit + 1 in int32: limits past 2^30 are refused
+        mut("split_limit_int32_max", lambda s: s.split_limit[0].__setitem__(1, 2147483647)),
+        mut("split_limit_2p30_plus_1", lambda s: s.split_limit[0].__setitem__(2, (1 << 30) + 1)),
     ]
     return v
 

@@ -15,6 +15,10 @@ def literal(x, s, amt, lim, sumcheck):
     s = list(s)
     rounds = 0
     while (not sumcheck or sum(x) > 0) and amt > 0:
+        if x[0] <= 0 and x[1] <= 0:
+            # no child eligible: every further round changes nothing, so the loop spins until the guard
+            # (taken in one jump: a 2^30 guard limit would otherwise loop 2^30 times here)
+            return x, s, amt, False
         for k in range(2):
             if x[k] > 0:
                 s[k] += 1
@@ -26,12 +30,17 @@ def literal(x, s, amt, lim, sumcheck):
     return x, s, amt, True
 
 
+def i32(v):
+    """C int32 wrap-around (the kernel's int arithmetic)."""
+    return ((v + 2 ** 31) % 2 ** 32) - 2 ** 31
+
+
 def closed(x, s, amt, lim, sumcheck):
-    """rr_closed<2> statement by statement (C integer semantics: >> is arithmetic)."""
+    """rr_closed<2> statement by statement (C int32 semantics: >> is arithmetic, lim + 1 wraps)."""
     x0, x1 = x
     s0, s1 = s
     go1 = amt > 0 and (not sumcheck or x0 + x1 > 0)
-    r1 = min(min(min(x0, x1), (amt + 1) >> 1), lim + 1)
+    r1 = min(min(min(x0, x1), (amt + 1) >> 1), i32(lim + 1))
     if not (go1 and x0 > 0 and x1 > 0):
         r1 = 0
     x0 -= r1
@@ -44,7 +53,7 @@ def closed(x, s, amt, lim, sumcheck):
     r2 = min(x0 if e0 else (x1 if e1 else 0), amt)
     if sumcheck:
         r2 = min(r2, x0 + x1)
-    r2 = min(r2, lim + 1 - r1)
+    r2 = min(r2, i32(i32(lim + 1) - r1))
     r2 = max(r2, 0) if go2 else 0
     r2a = r2 if e0 else 0
     r2b = r2 - r2a

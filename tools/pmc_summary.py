@@ -65,6 +65,10 @@ def main():
             line = line.strip()
             if line.startswith("{") and '"roofline"' in line:
                 rl = json.loads(line)["roofline"]
+                if rl["kernel"].startswith("jit-diag:"):
+                    # a diagnostic build (IMENV_ABLATE / IMENV_STAMPS: wrong results or extra stores) must never
+                    # stand in for the production kernel's traffic
+                    raise SystemExit("pmc_summary: refusing a diagnostic kernel build: " + rl["kernel"])
                 res["kernel_info"] = rl["kernel"]
                 res["algorithmic_bytes_per_launch"] = rl["bytes_per_launch"]
     fac = {}

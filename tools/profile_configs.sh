@@ -13,7 +13,7 @@ CMD="python tools/pmc_calib.py"; D=$OUT; run cal_fetch FETCH_SIZE && run cal_wri
 for cn in $CONFIGS; do
   c=${cn%%:*}; n=${cn##*:}
   D=$OUT/${c}_$n; mkdir -p $D
-  BENCH="python bench.py --config $c --n-envs $n --no-cpu-baseline --no-alt-store --steps 60 --warmup 30"
+  BENCH="python bench.py --config $c --n-envs $n --no-cpu-baseline --no-alt-store --no-alt-obs --steps 60 --warmup 30"
   timeout -k 10 240 $BENCH > $D/bench.json 2> $D/bench.err || exit 1
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$D/trace -o p --output-format csv -- $BENCH > $D/bench_trace.json 2> $D/trace.err || exit 1
   CMD=$BENCH

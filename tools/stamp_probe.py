@@ -4,7 +4,7 @@ s_memrealtime stamps at entry, loads issued, loads landed (an added vmcnt(0) wai
 barrier, stores issued, stores acknowledged). Prints the distribution of each phase over the waves and
 the launch's span, in microseconds (100 MHz counter).
 
-    IMENV_STAMPS=1 IMENV_JIT_OPTS=-DIMENV_STAMPS=1 python tools/stamp_probe.py --config C4 [--n-envs N] [--store S]
+    IMENV_DIAG=1 IMENV_STAMPS=1 IMENV_JIT_OPTS=-DIMENV_STAMPS=1 python tools/stamp_probe.py --config C4 [--n-envs N] [--store S]
 """
 import argparse
 import ctypes
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     args = ap.parse_args()
     assert os.environ.get("IMENV_STAMPS") == "1" and "IMENV_STAMPS" in os.environ.get("IMENV_JIT_OPTS", "")
+    assert os.environ.get("IMENV_DIAG") == "1", "a diagnostic kernel build needs IMENV_DIAG=1 (imenv_jit.hip)"
     import numpy as np
     import torch
     from bench import CONFIGS
@@ -56,6 +57,7 @@ def main():
             st = st[st[:, 0] > 0].astype(np.int64)
             rows.append(st)
     out = {"config": args.config, "n_envs": n, "kernel": env.kernel_info(), "store": args.store, "launches": []}
+    assert out["kernel"].startswith("jit-diag:"), out["kernel"]     # the stamps build, not an AOT fallback
     for st in rows:
         t0 = st[:, 0].min()
         d = np.diff(st[:, :7], axis=1) / 100.0       # 10 ns ticks -> us
