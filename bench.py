@@ -116,7 +116,19 @@ def cpu_baseline(seconds=1.5, cname="C2"):
                        env=env, capture_output=True, text=True, timeout=600)
     if r.returncode != 0:
         raise RuntimeError("cpu baseline failed: " + r.stderr[-2000:])
-    return json.loads(r.stdout.strip().splitlines()[-1])
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    # the port's speed relative to the reference's own step(), measured once where the reference exists
+    # (tools/cpu_ratio.py: one core, the same episodes), so the line can say what the
+    # reference itself would do on these cores
+    try:
+        with open(os.path.join(ROOT, "profiles", "cpu_ratio.json")) as f:
+            ratio = float(json.load(f)["configs"][cname]["port_over_reference"])
+        out.update(port_over_reference=ratio, reference_equiv_value=round(out["value"] / ratio, 1),
+                   ratio_source="profiles/cpu_ratio.json: the reference's environments/*.py step() and this port "
+                                "timed on the same episodes, one core, in the build container (tools/cpu_ratio.py)")
+    except (OSError, KeyError, ValueError):
+        pass
+    return out
 
 
 def _cpu_baseline_here(seconds, cname):

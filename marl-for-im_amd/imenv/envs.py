@@ -65,6 +65,34 @@ def rev_scale(val_scaled, min_val, max_val, A=-1, B=1):
     return ((val_scaled - A) * (max_val - min_val)) / (B - A) + min_val
 
 
+def make_spaces(kind, sp):
+    """(observation_space, action_space) of ONE env of the reference class `kind` (per agent for the
+    multi-agent classes): IM_env.py:60-139, MAIM_env.py:67-153, IM_div_env.py:95-180,
+    MAIM_div_env.py:103-218."""
+    N, F = sp.num_nodes, sp.num_features
+    ma = sp.multi_agent
+    a, b = sp.a, sp.b
+    inv_max = np.asarray(sp.inv_max, dtype=np.float64)
+    order_max = np.asarray(sp.order_max, dtype=np.float64)
+    obs_shape = (F,) if ma else (N, F)
+    if sp.standardise_state or kind == "MAIM_div":
+        obs_space = Box(low=np.ones(obs_shape) * a, high=np.ones(obs_shape) * b, dtype=np.float64, shape=obs_shape)
+    else:
+        # raw observations (IM_env.py:129-139, MAIM_env.py:138-153): inv, backlog (unbounded), order_u,
+        # then in-transit slots, all bounded by the largest capacity
+        m = float(np.max(inv_max))
+        high = np.full(obs_shape, m)
+        high[..., 1] = np.inf
+        obs_space = Box(low=np.zeros(obs_shape), high=high, dtype=np.float64, shape=obs_shape)
+    act_n = 1 if ma else N
+    if sp.standardise_actions or kind == "MAIM_div":
+        act_space = Box(low=np.ones(act_n) * a, high=np.ones(act_n) * b, dtype=np.float64, shape=(act_n,))
+    else:
+        high = np.ones(1) * np.max(order_max) if ma else order_max
+        act_space = Box(low=np.zeros(act_n), high=high, dtype=np.int32, shape=(act_n,))
+    return obs_space, act_space
+
+
 class _Adaptor:
     KIND = None
 
@@ -152,26 +180,7 @@ class _Adaptor:
         return int(depth.max()) + 1
 
     def _setup_spaces(self):
-        sp, N, F = self.spec, self.spec.num_nodes, self.spec.num_features
-        ma = sp.multi_agent
-        obs_shape = (F,) if ma else (N, F)
-        if sp.standardise_state or self.KIND == "MAIM_div":
-            self.observation_space = Box(low=np.ones(obs_shape) * self.a, high=np.ones(obs_shape) * self.b,
-                                         dtype=np.float64, shape=obs_shape)
-        else:
-            # raw observations (IM_env.py:129-139, MAIM_env.py:138-153): inv, backlog (unbounded), order_u,
-            # then in-transit slots, all bounded by the largest capacity
-            m = float(np.max(self.inv_max))
-            high = np.full(obs_shape, m)
-            high[..., 1] = np.inf
-            self.observation_space = Box(low=np.zeros(obs_shape), high=high, dtype=np.float64, shape=obs_shape)
-        act_n = 1 if ma else N
-        if sp.standardise_actions or self.KIND == "MAIM_div":
-            self.action_space = Box(low=np.ones(act_n) * self.a, high=np.ones(act_n) * self.b, dtype=np.float64,
-                                    shape=(act_n,))
-        else:
-            high = np.ones(1) * np.max(self.order_max) if ma else self.order_max
-            self.action_space = Box(low=np.zeros(act_n), high=high, dtype=np.int32, shape=(act_n,))
+        self.observation_space, self.action_space = make_spaces(self.KIND, self.spec)
 
     # ------------------------------------------------------------------ reference helpers
     def rescale(self, val, min_val, max_val, A=-1, B=1):
@@ -368,4 +377,4 @@ class MultiAgentInvManagementDiv(_MultiAgent):
 
 
 __all__ = ["InvManagement", "MultiAgentInvManagement", "InvManagementDiv", "MultiAgentInvManagementDiv",
-           "rescale", "rev_scale"]
+           "rescale", "rev_scale", "make_spaces"]

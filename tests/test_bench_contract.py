@@ -57,6 +57,9 @@ def test_bench_json_line(steps, warmup):
     # (58.7 MB of outputs per launch, more than L2) plain state rows; the informational run its own
     assert r["kernel"].startswith("jit:imenv_step_jit_wt[") and ",flags=0x2000," in r["kernel"]
     assert alt["kernel"].startswith("jit:imenv_step_jit[") and ",flags=0x0," in alt["kernel"]
+    f64 = r["alt_obs_f64"]           # the reference's float64 observations, same run (informational)
+    assert f64["kernel"].startswith("jit:imenv_step_jit_wt_o64[") and 0 < f64["frac"] < 1
+    assert f64["bytes_per_env_step"] > r["bytes_per_env_step"] and f64["value"] > 0
     g = r["graph"]                   # the HIP-graph-replayed episode (informational)
     assert g["steps"] == 30 * g["replays"] and g["ms_per_step"] > 0 and g["kernel"] == r["kernel"]
     assert d["resets_timed"] == sum(1 for s in range(warmup, warmup + steps) if s % 30 == 0)
