@@ -11,7 +11,7 @@ for ci in "${!CL[@]}"; do
     for v in "$@"; do
       name=${v%%=*}; asg=${v#*=}
       f=$OUT/c${ci}_${name}_$r
-      env "$asg" timeout -k 10 120 python bench.py --no-cpu-baseline --no-alt-store --no-graph ${CL[$ci]} > $f.json 2> $f.err || { echo "FAIL $f"; tail -5 $f.err; exit 1; }
+      env "$asg" timeout -k 10 120 python bench.py --no-cpu-baseline --no-alt-store --no-alt-obs --no-graph ${CL[$ci]} > $f.json 2> $f.err || { echo "FAIL $f"; tail -5 $f.err; exit 1; }
       python -c "import json; d=json.load(open('$f.json')); r=d['roofline']; print('${CL[$ci]}', '$name', d['value'], r['kernel_us'], r['frac'])"
     done
   done
