@@ -150,12 +150,14 @@ def _cpu_baseline_here(seconds, cname):
 
 
 # ----------------------------------------------------------------- PMC traffic
-def pmc_traffic(n_envs, kernel):
-    """HBM bytes per step-kernel launch from a committed rocprofv3 PMC summary of this exact kernel
-    variant (kernel_info) at this size: profiles/pmc_step_kernel.json (the metric's workload, written by
-    tools/profile_pmc.sh) or profiles/pmc_configs/*.json (the C3 / C4 configs, tools/profile_configs.sh),
-    else None."""
+def pmc_record(n_envs, kernel):
+    """The committed rocprofv3 summary of this exact kernel variant (kernel_info) at this size:
+    profiles/pmc_step_kernel.json (written by tools/profile_pmc.sh) or profiles/pmc_configs/*.json
+    (tools/profile_configs.sh: PMC passes + the kernel trace of the same bench command), else None.
+    A diagnostic build (tag "jit-diag:") never matches."""
     import glob
+    if kernel.startswith("jit-diag:"):
+        return None
     paths = [os.path.join(ROOT, "profiles", "pmc_step_kernel.json")]
     paths += sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_configs", "*.json")))
     for p in paths:
@@ -163,10 +165,17 @@ def pmc_traffic(n_envs, kernel):
             with open(p) as f:
                 d = json.load(f)
             if int(d.get("n_envs", -1)) == int(n_envs) and d.get("kernel_info") == kernel:
-                return float(d["hbm_bytes_per_launch"])
+                d["_path"] = os.path.relpath(p, ROOT)
+                return d
         except Exception:
             continue
     return None
+
+
+def pmc_traffic(n_envs, kernel):
+    """HBM bytes per step-kernel launch from the committed PMC summary of this kernel variant, else None."""
+    d = pmc_record(n_envs, kernel)
+    return float(d["hbm_bytes_per_launch"]) if d and "hbm_bytes_per_launch" in d else None
 
 
 # ----------------------------------------------------------------- launcher
@@ -645,6 +654,14 @@ def main():
         sys.stderr.write("bench.py: the timed kernel is a diagnostic build (%s): not a bench line\n" % kinfo)
     achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic = pmc_traffic(n, kinfo)
+    prof = pmc_record(n, kinfo)
+    trace = None
+    if prof and prof.get("trace_avg_ns"):
+        # the committed kernel trace of this kernel variant at this size, beside the live HIP-event time
+        tus = prof["trace_avg_ns"] / 1e3
+        trace = {"kernel_us": round(tus, 3), "min_us": round(prof.get("trace_min_ns", 0) / 1e3, 3),
+                 "calls": prof.get("trace_calls"), "frac": round(bytes_per_launch / (tus * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                 "source": prof["_path"]}
     launcher = os.environ.get("IMENV_BENCH_LAUNCHER", "external" if world > 1 else "none")
     size = "2^20" if global_envs == 1 << 20 else str(global_envs)
     if args.scaling == "strong":
@@ -702,6 +719,7 @@ def main():
             "alt_obs_f64": alt64,
             "graph": graph,
             "launch_pacing": spin_info or None,
+            "rocprof_trace": trace,
         },
         "gather": gather_info,
         "cpu_baseline": cpu,

@@ -5,6 +5,9 @@
 # variants interleaved; one line per run: config, variant, value, kernel us, frac.
 OUT=$1; R=$2; CFGS=$3; shift 3
 mkdir -p $OUT
+# a variant may build a diagnostic kernel (-DIMENV_ABLATE=..., e.g. the access-shape floor with no
+# arithmetic): allowed here, and bench.py marks such lines "diagnostic_build"
+export IMENV_DIAG=1
 IFS='|' read -ra CL <<< "$CFGS"
 for ci in "${!CL[@]}"; do
   for r in $(seq 1 $R); do

@@ -54,6 +54,11 @@ def main():
         i = argv.index("--bench-log")
         bench = argv[i + 1]
         del argv[i:i + 2]
+    trace = None
+    if "--trace" in argv:          # rocprofv3 --kernel-trace --stats CSV of the same bench command
+        i = argv.index("--trace")
+        trace = argv[i + 1]
+        del argv[i:i + 2]
     outp = argv[0]
     n_envs = int(argv[1])
     s = load(argv[2:])
@@ -87,6 +92,14 @@ def main():
             res.update(kernel=k, hbm_read_bytes_per_launch=rd, hbm_write_bytes_per_launch=wr,
                        hbm_bytes_per_launch=rd + wr,
                        raw_fetch_kb=c["FETCH_SIZE"], raw_write_kb=c["WRITE_SIZE"])
+    if trace and res.get("kernel"):
+        import csv
+        for row in csv.DictReader(open(trace)):
+            if row["Name"].strip('"') == res["kernel"]:
+                # the kernel trace's own average duration of the same kernel, for bench.py to print next
+                # to its HIP-event time (sub-5 us kernels read high under the trace: profiles/INDEX.md)
+                res.update(trace_avg_ns=float(row["AverageNs"]), trace_min_ns=float(row["MinNs"]),
+                           trace_calls=int(row["Calls"]))
     with open(outp, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
     print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))

@@ -21,7 +21,7 @@ for cn in $CONFIGS; do
   run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY &&
   run sq2 SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_WAIT_INST_LDS &&
   run tcc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE || exit 1
-  python tools/pmc_summary.py $D/summary.json $n $OUT/cal_fetch $OUT/cal_write $D/fetch $D/write $D/sq1 $D/sq2 $D/tcc --bench-log $D/fetch.log > $D/summary.log 2>&1 || exit 1
+  python tools/pmc_summary.py $D/summary.json $n $OUT/cal_fetch $OUT/cal_write $D/fetch $D/write $D/sq1 $D/sq2 $D/tcc --bench-log $D/fetch.log --trace $D/trace/p_kernel_stats.csv > $D/summary.log 2>&1 || exit 1
   echo "$c $n done"
 done
 echo "profile_configs done"
