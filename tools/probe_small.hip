@@ -93,6 +93,44 @@ __global__ void __launch_bounds__(BS) probe_fp(const PSArgs A) {
   }
 }
 
+// The same per-env bytes with the state held as ONE 16-byte record per env (net row 4 B, order_u row
+// 4 B, the 7 ring slots + 1 pad byte): one dwordx4 load and one dwordx4 store per lane instead of
+// 2 dword + 4 byte loads and stores. Reads 16 + 16 B, writes 16 + 48 + 8 B = 104 B per env.
+template <int BS>
+__global__ void __launch_bounds__(BS) probe_aos16(const PSArgs A) {
+  __shared__ __attribute__((aligned(16))) float s_obs[BS * 12];
+  const int tid = threadIdx.x;
+  const int64_t e0 = (int64_t)blockIdx.x * BS;
+  const int64_t e = e0 + tid;
+  const float4 a = A.act[e];
+  uint4* st = reinterpret_cast<uint4*>(A.net);      // [n] records (the net buffer is 16 B per env here)
+  const uint4 v = st[e];
+  const uint32_t s = v.x + v.y + (v.z & 0xFF) + (v.w >> 24) + (uint32_t)(int)a.x;
+  const float f = (float)s;
+#pragma unroll
+  for (int q = 0; q < 12; ++q) s_obs[tid * 12 + q] = f + (float)q * a.y;
+  const double rw = (double)s * a.z;
+  const int64_t u0 = uniform(e0);
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  u4 w = {v.x + s, v.y ^ s, v.z + s, v.w - s};
+  __builtin_amdgcn_raw_buffer_store_b128(w, rsrc(st + u0), 16 * tid, 0, kSC1);
+  if constexpr (BS > 64) __syncthreads();
+  else __builtin_amdgcn_wave_barrier();
+  const float4* s4 = reinterpret_cast<const float4*>(s_obs);
+  const auto ro = rsrc(A.obs + u0 * 12);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const float4 x = s4[q * BS + tid];
+    u4 ww;
+    __builtin_memcpy(&ww, &x, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(ww, ro, (q * BS + tid) * 16, 0, kSC1);
+  }
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  u2 w2;
+  __builtin_memcpy(&w2, &rw, 8);
+  __builtin_amdgcn_raw_buffer_store_b64(w2, rsrc(A.rew + u0), tid * 8, 0, kSC1);
+}
+
 extern "C" int probe_small_run(int which, const PSArgs* A, void* stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t n = A->n;
@@ -102,6 +140,8 @@ extern "C" int probe_small_run(int which, const PSArgs* A, void* stream) {
     case 2: probe_fp<64, true><<<(unsigned)(n / 64), 64, 0, st>>>(*A); break;
     case 3: probe_fp<256, true><<<(unsigned)(n / 256), 256, 0, st>>>(*A); break;
     case 4: probe_empty<256><<<(unsigned)(n / 256), 256, 0, st>>>(*A); break;
+    case 5: probe_aos16<64><<<(unsigned)(n / 64), 64, 0, st>>>(*A); break;
+    case 6: probe_aos16<256><<<(unsigned)(n / 256), 256, 0, st>>>(*A); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;

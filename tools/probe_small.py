@@ -20,7 +20,8 @@ ROOT = os.path.dirname(HERE)
 sys.path[:0] = [ROOT, os.path.join(ROOT, "marl-for-im_amd")]
 SRC = os.path.join(HERE, "probe_small.hip")
 LIB = os.path.join(HERE, "bin", "libprobe_small.so")
-NAMES = ["empty_bs64", "footprint_plain_bs64", "footprint_wt_bs64", "footprint_wt_bs256", "empty_bs256"]
+NAMES = ["empty_bs64", "footprint_plain_bs64", "footprint_wt_bs64", "footprint_wt_bs256", "empty_bs256",
+         "aos16_wt_bs64", "aos16_wt_bs256"]
 
 
 class PSArgs(ctypes.Structure):
@@ -56,7 +57,7 @@ def main():
     lib = ctypes.CDLL(LIB)
     lib.probe_small_run.argtypes = [ctypes.c_int, ctypes.POINTER(PSArgs), ctypes.c_void_p]
     act = torch.rand((T, n, 4), device=dev) * 2 - 1
-    st = torch.zeros((2, n), dtype=torch.int32, device=dev)
+    st = torch.zeros((4, n), dtype=torch.int32, device=dev)       # aos16 uses all 16 B per env of row 0..
     ring = torch.zeros((7, n), dtype=torch.uint8, device=dev)
     obs = torch.zeros((T, n, 4, 3), dtype=torch.float32, device=dev)
     rew = torch.zeros((T, n), dtype=torch.float64, device=dev)
@@ -102,7 +103,8 @@ def main():
             episode(k, ev)
             ev[1].synchronize()
             times[names[k]].append(ev[0].elapsed_time(ev[1]) * 1e3 / (T - 1))
-    out = {"n_envs": n, "kernel": env.kernel_info(), "bytes_per_env": 96, "us_per_launch": {}, "frac_96B": {}}
+    out = {"n_envs": n, "kernel": env.kernel_info(), "bytes_per_env": 96, "us_per_launch": {}, "frac_96B": {},
+           "note": "aos16_* move 104 B per env (16-byte state records); frac_96B prices every variant at 96 B"}
     for k in names:
         us = float(np.median(times[k]))
         out["us_per_launch"][k] = round(us, 3)
