@@ -67,7 +67,8 @@ typedef unsigned long long uint64_t;
 #endif
 // Ablations (diagnostic builds only, WRONG results: timing where the compute goes): bit 0 skips the
 // divergent split, bit 1 the demand draw (Philox + Poisson), bit 2 computes observations as (float)v,
-// bit 3 skips profit / reward arithmetic, bit 4 skips the order decode (order = 0).
+// bit 3 skips profit / reward arithmetic, bit 4 skips the order decode (order = 0), bit 5 replaces the
+// scalar load of the device episode word by 0.
 #ifndef IMENV_ABLATE
 #define IMENV_ABLATE 0
 #endif
@@ -1182,7 +1183,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   const int np = p.np();
   const int t = A.t;
   const bool poisson = p.demand_layout() == IMENV_LAYOUT_DRAW && p.demand_dist() == IMENV_DEMAND_POISSON;
-  const uint32_t ep = *A.episode;
+  const uint32_t ep = (IMENV_ABLATE & 32) ? 0u : *A.episode;   // (diagnostic: no scalar load of the episode word)
   const uint32_t gid = A.env_offset + (uint32_t)e;
   const uint64_t seed = p.seed();
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);

@@ -13,8 +13,12 @@
 #   pmc:C:N          PMC passes at config C, N envs (tools/profile_configs.sh), summary under OUT/pmc
 #   probe_small:N    tools/probe_small.py floors at N envs, plus its kernel trace
 #   stamps:C:N       per-wave phase stamps of a diagnostic build (tools/stamp_probe.py)
-#   rehearse         bench.py --gpus 2 --rehearse-one-gpu (plain and --gather)
+#   rehearse[:N]     bench.py --gpus N (default 2) --rehearse-one-gpu: every rank on GPU 0 with gloo, the
+#                    strong-scaled shards and the gather pass (plain, then --no-gather)
 #   py:SCRIPT[:ARGS] any python tool, ARGS comma-separated (its stdout to OUT/<script>.log)
+#   floors:R         interleaved A/B (tools/ab_multi.sh, R rounds) of the production step kernel, its
+#                    access-shape floor (IMENV_ABLATE=63: the same loads and stores, no arithmetic) and
+#                    128-env blocks with wave-local write-out, at C4 / C3 / C2 131,072 / C2 2^20
 OUT=${1:?usage: gpu.sh OUTDIR TASK...}
 shift
 export TMPDIR=/tmp
@@ -68,11 +72,19 @@ for task in "$@"; do
         --n-envs "$b" > "$OUT/stamps_${a}_$b.json" 2> "$OUT/stamps_${a}_$b.err" || fail stamps "$OUT/stamps_${a}_$b.err"
       echo "stamps $a $b ok" ;;
     rehearse)
-      timeout -k 10 300 python bench.py --gpus 2 --rehearse-one-gpu --steps 20 --warmup 5 > "$OUT/rehearse2.json" \
-        2> "$OUT/rehearse2.err" || fail rehearse "$OUT/rehearse2.err"
-      timeout -k 10 300 python bench.py --gpus 2 --rehearse-one-gpu --gather --steps 60 --warmup 10 --no-cpu-baseline \
-        > "$OUT/rehearse2_gather.json" 2> "$OUT/rehearse2_gather.err" || fail "rehearse gather" "$OUT/rehearse2_gather.err"
-      echo "rehearse ok" ;;
+      w=${a:-2}
+      timeout -k 10 300 python bench.py --gpus "$w" --rehearse-one-gpu --steps 20 --warmup 5 > "$OUT/rehearse$w.json" \
+        2> "$OUT/rehearse$w.err" || fail rehearse "$OUT/rehearse$w.err"
+      timeout -k 10 300 python bench.py --gpus "$w" --rehearse-one-gpu --no-gather --steps 60 --warmup 10 --no-cpu-baseline \
+        > "$OUT/rehearse${w}_nogather.json" 2> "$OUT/rehearse${w}_nogather.err" || fail "rehearse no-gather" "$OUT/rehearse${w}_nogather.err"
+      echo "rehearse $w ok" ;;
+    floors)
+      timeout -k 10 1500 bash tools/ab_multi.sh "$OUT/floors" "$a" \
+        "--config C4|--config C3|--config C2 --n-envs 131072|--config C2 --steps 60 --warmup 30" \
+        "base=IMENV_AB=0" "floor=IMENV_JIT_OPTS=-DIMENV_ABLATE=63" "noep=IMENV_JIT_OPTS=-DIMENV_ABLATE=32" \
+        "bs128ws=IMENV_JIT_BS=128;IMENV_JIT_OPTS=-DIMENV_WAVE_SLAB=1" > "$OUT/floors.log" 2>&1 \
+        || fail floors "$OUT/floors.log"
+      echo "floors ok" ;;
     py)
       s=$(basename "$a" .py)
       b=${b//,/ }
