@@ -70,9 +70,10 @@ class _Batch:
         # one float64 and one int32 device buffer, each copied to pinned host memory once per step
         self._dev_f = torch.empty(n * N * F + n * self.nr + n * N, dtype=torch.float64, device=dev)
         self._dev_i = torch.empty(6 * n * N, dtype=torch.int32, device=dev)
-        self._host_f = torch.empty(self._dev_f.shape, dtype=torch.float64, pin_memory=True)
-        self._host_i = torch.empty(self._dev_i.shape, dtype=torch.int32, pin_memory=True)
-        self._host_a = torch.empty((n, N), dtype=torch.float64, pin_memory=True)
+        pin = dev.type == "cuda"     # (the CPU tests drive this class over an oracle-backed stand-in)
+        self._host_f = torch.empty(self._dev_f.shape, dtype=torch.float64, pin_memory=pin)
+        self._host_i = torch.empty(self._dev_i.shape, dtype=torch.int32, pin_memory=pin)
+        self._host_a = torch.empty((n, N), dtype=torch.float64, pin_memory=pin)
         self._dev_a = torch.empty((n, N), dtype=torch.float64, device=dev)
         f, i = self._dev_f, self._dev_i
         self._obs = f[:n * N * F].view(n, N, F)
@@ -89,7 +90,8 @@ class _Batch:
         self._host_f.copy_(self._dev_f, non_blocking=True)
         if what:
             self._host_i.copy_(self._dev_i, non_blocking=True)
-        torch.cuda.current_stream(self.env.device).synchronize()
+        if self.env.device.type == "cuda":
+            torch.cuda.current_stream(self.env.device).synchronize()
 
     def reset_all(self):
         """One batched reset: every env to period 0; returns host observations [n, N, F] (float64)."""
