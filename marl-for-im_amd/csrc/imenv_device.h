@@ -191,6 +191,8 @@ struct StepArgs {
   uint64_t* stamps;           // diagnostics (IMENV_STAMPS builds): [waves][8] s_memrealtime phase stamps, or null
   int64_t n;
   uint32_t env_offset;
+  uint32_t episode_val;       // the device episode word's value, known on the host for eager launches
+                              // (P::EP_ARG kernels take it from here: no dependent scalar load)
   int32_t t;
   int32_t action_f64;
   int32_t obs_f64;
@@ -592,6 +594,7 @@ struct DynSpec {
   static constexpr bool OBS_STAGE64 = false;         // float64 observations are stored directly
   static constexpr int TD_PRE = 0;                   // in-transit obs slots are loaded after the step
   static constexpr bool XCD_REMAP = false;           // (step_body)
+  static constexpr bool EP_ARG = false;              // the episode word is read from device memory
   using ST = ST_;
   const SpecDev* __restrict__ sp;
   const StepArgs& A;
@@ -1183,7 +1186,9 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   const int np = p.np();
   const int t = A.t;
   const bool poisson = p.demand_layout() == IMENV_LAYOUT_DRAW && p.demand_dist() == IMENV_DEMAND_POISSON;
-  const uint32_t ep = (IMENV_ABLATE & 32) ? 0u : *A.episode;   // (diagnostic: no scalar load of the episode word)
+  // the episode word: a kernel argument when the host knows its value (eager launches: P::EP_ARG),
+  // else the device word the reset kernel advances (graph-captured launches replay with fresh values)
+  const uint32_t ep = (IMENV_ABLATE & 32) ? 0u : (P::EP_ARG ? A.episode_val : *A.episode);
   const uint32_t gid = A.env_offset + (uint32_t)e;
   const uint64_t seed = p.seed();
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
