@@ -5,7 +5,9 @@
 #   /usr/local/graft/bin/gpurun --timeout 900 -- bash tools/gpu.sh gpurun_out/r4x tests smoke bench
 #
 # Tasks:
-#   tests            the whole GPU suite (pytest -m gpu)
+#   tests            the whole GPU suite (pytest -m gpu -x)
+#   tests_all        the whole GPU suite without -x (every failure listed; test failures do not stop
+#                    the script, a crash or time limit does)
 #   smoke            __graft_entry__.smoke()
 #   bench            bench.py at the driver's settings (--steps 20 --warmup 5) and at its defaults
 #   trace            rocprofv3 --kernel-trace --stats of the default bench command
@@ -35,6 +37,11 @@ for task in "$@"; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
         > "$OUT/pytest_gpu.log" 2>&1 || fail tests "$OUT/pytest_gpu.log"
       tail -n 1 "$OUT/pytest_gpu.log" ;;
+    tests_all)
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread \
+        > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+      tail -n 3 "$OUT/pytest_gpu.log"
+      [ $rc -le 1 ] || fail "tests_all rc=$rc" "$OUT/pytest_gpu.log" ;;
     smoke)
       timeout -k 10 180 python __graft_entry__.py smoke > "$OUT/smoke.log" 2>&1 || fail smoke "$OUT/smoke.log"
       echo "smoke ok" ;;
