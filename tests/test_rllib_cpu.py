@@ -138,3 +138,12 @@ def test_reset_rounds(cpu_batch):
     env.vector_step([d["actions"][i, 0] for i in range(E)])
     with pytest.raises(RuntimeError):
         env.reset_at(0)
+
+
+@pytest.mark.parametrize("kind,cfg_name", [("IM", "C1_IM4"), ("MAIM_div", "C4_MAIM_div1")])
+def test_oracle_episode_sequence_on_the_stand_in(cpu_batch, kind, cfg_name, monkeypatch):
+    """tests/test_rllib_gpu.py's 64-env, two-episode oracle comparison, run here over the stand-in
+    (the sequence and the shapes it feeds the oracle are checked on CPU before the GPU runs it)."""
+    import test_rllib_gpu as g
+    monkeypatch.setattr(g, "DEV", "cpu")
+    g.test_batched_surfaces_match_the_oracle_over_episodes(kind, cfg_name)

@@ -108,7 +108,7 @@ def test_batched_surfaces_match_the_oracle_over_episodes(kind, cfg_name):
     E = 64
     rs = np.random.RandomState(7)
     ora = OracleEnv(kind, cfg, n_envs=E)
-    N, T, R = ora.N, ora.T, len(ora.retailers)
+    N, T, R = ora.N, ora.num_periods, len(ora.retailers)
     serial = kind in ("IM", "MAIM")
     demands = [rs.poisson(5, (E, T) if serial else (E, R, T)) for _ in range(2)]
     acts = [rs.uniform(-1, 1, (T, E, N)) for _ in range(2)]
