@@ -691,10 +691,6 @@ struct ImEnv {
   std::vector<double> lut64;
   uint32_t *d_err = nullptr, *d_err_any = nullptr;
   uint32_t* d_episode = nullptr;
-  // host mirror of the device episode word (known unless a reset was graph-captured: a replay advances
-  // the device word without the host seeing it); eager step launches then pass it as an argument
-  bool ep_known = true;
-  uint32_t ep_val = 0xFFFFFFFFu;
   int t = 0;
   bool reset_done = false;
   bool noisy_delay = false;
@@ -855,13 +851,6 @@ int imenv_reset(ImEnv* h, const int32_t* demand, int demand_layout, int noisy_de
   }
   h->t = 0;
   h->reset_done = true;
-  {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(st, &cs);
-    if (cs != hipStreamCaptureStatusNone) h->ep_known = false;           // replays advance it unseen
-    else if (episode >= 0) { h->ep_known = true; h->ep_val = (uint32_t)episode; }
-    else h->ep_val += 1u;                                                 // as the reset kernel does
-  }
   int64_t blocks = ((int64_t)n + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(imenv_reset_kernel, dim3((unsigned)blocks), dim3(256), 0, st, h->d_spec, obs,
@@ -935,33 +924,17 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
     f.wt_state = h->store_policy == IMENV_STORE_WRITETHROUGH ||
                  (h->store_policy == IMENV_STORE_DEFAULT && wt_state_pays(s, h->n, A.obs_f64 != 0));
     f.small_blocks = h->n <= kSmallLaunchEnvs;
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(st, &cap);
-    // eager launches with a known episode word take it as an argument (no dependent scalar load at
-    // the start of the kernel); captured launches read the device word, which replays advance
-    f.ep_arg = cap == hipStreamCaptureStatusNone && h->ep_known && !std::getenv("IMENV_EP_DEVICE");
-    A.episode_val = h->ep_val;
     auto it = h->jit_k.find(f.key());
     if (it == h->jit_k.end()) {
       // compiling + loading a module is not stream work: never do it while the stream is being
       // captured into a graph (that launch takes the ahead-of-time kernel instead)
-      if (cap == hipStreamCaptureStatusNone) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      (void)hipStreamIsCapturing(st, &cs);
+      if (cs == hipStreamCaptureStatusNone) {
         imenv::JitKernel k;
         std::string msg;
         if (imenv::jit_load(h->host, h->maxc, c.base, f, h->arch, k, msg)) {
           it = h->jit_k.emplace(f.key(), k).first;
-          if (f.ep_arg) {
-            // the device-word sibling too, now: a later graph capture of this flag set needs it and
-            // cannot compile or load a module while the stream is capturing
-            imenv::JitFlags f2 = f;
-            f2.ep_arg = false;
-            if (h->jit_k.find(f2.key()) == h->jit_k.end()) {
-              imenv::JitKernel k2;
-              std::string msg2;
-              if (imenv::jit_load(h->host, h->maxc, c.base, f2, h->arch, k2, msg2)) h->jit_k.emplace(f2.key(), k2);
-              it = h->jit_k.find(f.key());
-            }
-          }
         } else {
           h->jit_err = msg;
           if (h->jit_strict) return fail(IMENV_E_UNSUPPORTED, "JIT step kernel: " + msg);
@@ -1433,7 +1406,6 @@ int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, cha
   f.wt_obs = flags & 8192u;
   f.wt_state = flags & 16384u;
   f.small_blocks = flags & 32768u;
-  f.ep_arg = flags & 65536u;
   f.demand_layout = (int)((flags >> 5) & 31u);
   std::string msg;
   std::string src;

@@ -67,8 +67,9 @@ typedef unsigned long long uint64_t;
 #endif
 // Ablations (diagnostic builds only, WRONG results: timing where the compute goes): bit 0 skips the
 // divergent split, bit 1 the demand draw (Philox + Poisson), bit 2 computes observations as (float)v,
-// bit 3 skips profit / reward arithmetic, bit 4 skips the order decode (order = 0), bit 5 replaces the
-// scalar load of the device episode word by 0.
+// bit 3 skips profit / reward arithmetic, bit 4 skips the order decode (order = the action's sign bit:
+// the action load stays), bit 5 replaces the scalar load of the device episode word by 0. Every
+// ablation keeps every load and store, so IMENV_ABLATE=63 is the access-shape floor of the kernel.
 #ifndef IMENV_ABLATE
 #define IMENV_ABLATE 0
 #endif
@@ -191,8 +192,6 @@ struct StepArgs {
   uint64_t* stamps;           // diagnostics (IMENV_STAMPS builds): [waves][8] s_memrealtime phase stamps, or null
   int64_t n;
   uint32_t env_offset;
-  uint32_t episode_val;       // the device episode word's value, known on the host for eager launches
-                              // (P::EP_ARG kernels take it from here: no dependent scalar load)
   int32_t t;
   int32_t action_f64;
   int32_t obs_f64;
@@ -594,7 +593,6 @@ struct DynSpec {
   static constexpr bool OBS_STAGE64 = false;         // float64 observations are stored directly
   static constexpr int TD_PRE = 0;                   // in-transit obs slots are loaded after the step
   static constexpr bool XCD_REMAP = false;           // (step_body)
-  static constexpr bool EP_ARG = false;              // the episode word is read from device memory
   using ST = ST_;
   const SpecDev* __restrict__ sp;
   const StepArgs& A;
@@ -733,7 +731,8 @@ __device__ __forceinline__ void decode_orders(const P& p, const double (&x)[P::N
         v = fold ? d * (om * ib) : (ib != 0.0 ? (d * om) * ib : (d * om) / bma);
       }
       const double o = p.clip_round() ? rint(fmin(fmax(v, 0.0), om)) : fmin(fmax(rint(v), 0.0), om);
-      order[i] = (IMENV_ABLATE & 16) ? 0 : (int)o;
+      // (the ablation keeps the action load: order 0 or 1 from the action's sign, no decode arithmetic)
+      order[i] = (IMENV_ABLATE & 16) ? (x[i] > 0.0 ? 1 : 0) : (int)o;
     }
   }
 }
@@ -1186,9 +1185,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   const int np = p.np();
   const int t = A.t;
   const bool poisson = p.demand_layout() == IMENV_LAYOUT_DRAW && p.demand_dist() == IMENV_DEMAND_POISSON;
-  // the episode word: a kernel argument when the host knows its value (eager launches: P::EP_ARG),
-  // else the device word the reset kernel advances (graph-captured launches replay with fresh values)
-  const uint32_t ep = (IMENV_ABLATE & 32) ? 0u : (P::EP_ARG ? A.episode_val : *A.episode);
+  const uint32_t ep = (IMENV_ABLATE & 32) ? 0u : *A.episode;   // (diagnostic: no scalar load of the episode word)
   const uint32_t gid = A.env_offset + (uint32_t)e;
   const uint64_t seed = p.seed();
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);

@@ -33,12 +33,11 @@ struct JitFlags {
   bool wt_obs = false;        // write-through (sc1) observation / reward stores
   bool wt_state = false;      // write-through (sc1) state-row stores
   bool small_blocks = false;  // a launch of at most two waves per SIMD: 64-env blocks (imenv_jit.hip)
-  bool ep_arg = false;        // the episode word comes as a kernel argument (StepArgs::episode_val)
   uint32_t key() const {
     return (act_f64 ? 1u : 0u) | (obs_f64 ? 2u : 0u) | (noisy_delay ? 4u : 0u) | (noisy_demand ? 8u : 0u) |
            (has_delay_u ? 16u : 0u) | ((uint32_t)demand_layout << 5) | (metrics ? 1024u : 0u) |
            (stream_store ? 2048u : 0u) | (wt_obs ? 8192u : 0u) | (wt_state ? 16384u : 0u) |
-           (small_blocks ? 32768u : 0u) | (ep_arg ? 65536u : 0u);
+           (small_blocks ? 32768u : 0u);
   }
 };
 

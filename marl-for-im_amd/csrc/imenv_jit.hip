@@ -318,7 +318,6 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
     << "  static constexpr bool OBS_STAGE64 = " << blit(f.obs_f64) << ";\n"
     << "  static constexpr int TD_PRE = " << (has_td && d.dmax > 1 ? d.dmax - 1 : 0) << ";\n"
     << "  static constexpr bool XCD_REMAP = " << blit(f.small_blocks) << ";\n"
-    << "  static constexpr bool EP_ARG = " << blit(f.ep_arg) << ";\n"
     << "  using ST = " << (d.es == 1 ? "uint8_t" : d.es == 2 ? "int16_t" : "int32_t") << ";\n"
     << "  const imenv::SpecDev* __restrict__ sp;\n"
     << "  template <class X> __device__ JitSpec(const imenv::SpecDev* __restrict__ s, const X&) : sp(s) {}\n";

@@ -65,7 +65,6 @@ def test_jit_specialiser_compiles_every_golden_spec():
         sets = [0, 1 | 2 | (_native.LAYOUT_PER_ENV << 5) | (16 if meta["noisy"] else 0) | 1024]
         if name in ("C2_MAIM4", "C3_IM8", "C4_MAIM_div1", "MAIM_div2_share", "IM4_td_pd_pa_L2"):
             sets += [2048, 2 | 2048]          # streaming stores (IMENV_STORE_STREAM), f32 and f64 obs
-            sets += [0x12000, 0x1e000]        # eager launches: episode word as an argument (+ small blocks)
         for flags in sets:
             rc = lib.imenv_jit_check(ctypes.byref(spec), b"gfx950", flags, log, len(log))
             assert rc == 0, (name, flags, log.value.decode()[:2000])

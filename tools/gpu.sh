@@ -18,11 +18,11 @@
 #   rehearse[:N]     bench.py --gpus N (default 2) --rehearse-one-gpu: every rank on GPU 0 with gloo, the
 #                    strong-scaled shards and the gather pass (plain, then --no-gather)
 #   py:SCRIPT[:ARGS] any python tool, ARGS comma-separated (its stdout to OUT/<script>.log)
-#   floors:R         interleaved A/B (tools/ab_multi.sh, R rounds) of the production step kernel, its
-#                    access-shape floor (IMENV_ABLATE=63: the same loads and stores, no arithmetic), no
-#                    episode load at all (ABLATE=32), the episode word read from device memory
-#                    (IMENV_EP_DEVICE=1: round 3's kernel) and 128-env blocks with wave-local write-out,
-#                    at C4 / C3 / C2 131,072 / C2 2^20
+#   floors:R         interleaved A/B (tools/ab_multi.sh, R rounds) of the production step kernel and its
+#                    access-shape floor (IMENV_ABLATE=63: the same vector loads and stores, no
+#                    arithmetic) at C4 / C3 / C2 131,072 / C2 2^20
+#   ablate:R         the production kernel beside each ablation alone (decode, split, draw, obs, profit)
+#                    and all of them, at C4 and C2 131,072
 OUT=${1:?usage: gpu.sh OUTDIR TASK...}
 shift
 export TMPDIR=/tmp
@@ -90,11 +90,15 @@ for task in "$@"; do
     floors)
       timeout -k 10 1500 bash tools/ab_multi.sh "$OUT/floors" "$a" \
         "--config C4|--config C3|--config C2 --n-envs 131072|--config C2 --steps 60 --warmup 30" \
-        "base=IMENV_AB=0" "floor=IMENV_JIT_OPTS=-DIMENV_ABLATE=63" "noep=IMENV_JIT_OPTS=-DIMENV_ABLATE=32" \
-        "epdev=IMENV_EP_DEVICE=1" \
-        "bs128ws=IMENV_JIT_BS=128;IMENV_JIT_OPTS=-DIMENV_WAVE_SLAB=1" > "$OUT/floors.log" 2>&1 \
+        "base=IMENV_AB=0" "floor=IMENV_JIT_OPTS=-DIMENV_ABLATE=63" > "$OUT/floors.log" 2>&1 \
         || fail floors "$OUT/floors.log"
       echo "floors ok" ;;
+    ablate)
+      timeout -k 10 1500 bash tools/ab_multi.sh "$OUT/ablate" "$a" "--config C4|--config C2 --n-envs 131072" \
+        "base=IMENV_AB=0" "a63=IMENV_JIT_OPTS=-DIMENV_ABLATE=63" "a16=IMENV_JIT_OPTS=-DIMENV_ABLATE=16" \
+        "a1=IMENV_JIT_OPTS=-DIMENV_ABLATE=1" "a2=IMENV_JIT_OPTS=-DIMENV_ABLATE=2" "a4=IMENV_JIT_OPTS=-DIMENV_ABLATE=4" \
+        "a8=IMENV_JIT_OPTS=-DIMENV_ABLATE=8" > "$OUT/ablate.log" 2>&1 || fail ablate "$OUT/ablate.log"
+      echo "ablate ok" ;;
     py)
       s=$(basename "$a" .py)
       b=${b//,/ }
