@@ -19,7 +19,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "marl-for-im_amd")]
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--sizes", default="64,1024,16384")
+    ap.add_argument("--sizes", nargs="+", default=["64,1024,16384"])   # "64,1024" or "64 1024"
     ap.add_argument("--episodes", type=int, default=3)
     args = ap.parse_args()
     import numpy as np
@@ -28,7 +28,7 @@ def main():
     from imenv.rllib import InvMultiAgentBaseEnv, InvVectorEnv
     cfg = bench.CONFIGS["C2"][1]
     rs = np.random.RandomState(0)
-    for n in [int(x) for x in args.sizes.split(",")]:
+    for n in [int(x) for part in args.sizes for x in part.split(",") if x]:
         for cls, kind in ((InvMultiAgentBaseEnv, "MAIM"), (InvVectorEnv, "IM")):
             env = cls(kind, dict(cfg), num_envs=n)
             steps = 0
