@@ -180,11 +180,12 @@ class InvVectorEnv(_VectorEnv):
         obs, rew, info, t = self._b.step(actions)
         n = self.num_envs
         done = self._b.done
-        obs_l = [obs[i].copy() for i in range(n)]
-        rew_l = [float(rew[i]) for i in range(n)]
+        obs_l = list(obs.copy())                # per-env views of one fresh copy (the host mirror is reused)
+        rew_l = rew.tolist()
         if info is not None:
-            infos = [{"period": t, "demand": info["demand"][i], "ship": info["ship"][i],
-                      "acquisition": info["acquisition"][i], "profit": info["profit"][i]} for i in range(n)]
+            dem, shp, acq, pro = (list(info[k]) for k in ("demand", "ship", "acquisition", "profit"))
+            infos = [{"period": t, "demand": dem[i], "ship": shp[i], "acquisition": acq[i], "profit": pro[i]}
+                     for i in range(n)]
         else:
             infos = [{} for _ in range(n)]
         return obs_l, rew_l, [done] * n, infos
@@ -256,15 +257,14 @@ class InvMultiAgentBaseEnv(_BaseEnv):
                 rew, done, info = lr, ld, li
                 self._last_rew[i], self._last_done[i], self._last_info[i] = {}, {}, {}
                 self._obs[i] = {}
+            elif obs:
+                # the observation holds every agent of the env, so every pending agent entry is
+                # released: the pending dicts themselves are handed out and start over empty
+                rew, done, info = lr, ld, li
+                done["__all__"] = False
+                self._last_rew[i], self._last_done[i], self._last_info[i] = {}, {}, {}
             else:
                 rew, done, info = {}, {"__all__": False}, {}
-                for ag in obs:
-                    if ag in lr:
-                        rew[ag] = lr.pop(ag)
-                    if ag in ld:
-                        done[ag] = ld.pop(ag)
-                    if ag in li:
-                        info[ag] = li.pop(ag)
             self._last_done[i]["__all__"] = False
             obs_d[i], rew_d[i], done_d[i], info_d[i] = obs, rew, done, info
         return obs_d, rew_d, done_d, info_d, {}
@@ -278,32 +278,44 @@ class InvMultiAgentBaseEnv(_BaseEnv):
         if len(action_dict) != n:
             raise ValueError("the batch steps its %d envs in lockstep: actions for every env are needed (got %d)"
                              % (n, len(action_dict)))
-        act = np.empty((n, self._b.N), dtype=np.float64)
-        for env_id, ad in action_dict.items():
-            for k, ag in enumerate(self.agent_ids):
-                act[int(env_id), k] = float(np.asarray(ad[ag], dtype=np.float64).reshape(-1)[0])
+        ids, N = self.agent_ids, self._b.N
+        try:
+            flat = [action_dict[i][ag] for i in range(n) for ag in ids]
+        except KeyError as e:
+            raise ValueError("actions for env ids 0..%d and agents %s are needed (missing %r)" % (n - 1, ids, e.args[0]))
+        try:
+            act = np.asarray(flat, dtype=np.float64).reshape(n, N)     # one scalar or 1-element array each
+        except ValueError:
+            act = np.array([float(np.asarray(x, dtype=np.float64).reshape(-1)[0]) for x in flat]).reshape(n, N)
         obs, rew, info, t = self._b.step(act)
         done = self._b.done
-        indep = self._b.nr == self._b.N
         period = t + 1
+        rows = list(obs.copy().reshape(n * N, -1))     # per-agent views of one fresh copy
+        rv = list(rew.ravel())                         # np.float64 scalars: [n] shared or [n, N] per agent
+        indep = len(rv) == n * N
+        if info is not None:            # one info dict per (env, agent), env-major
+            infs = [{"period": period, "demand": d, "ship": s, "acquisition": a, "actual order": o, "profit": p}
+                    for d, s, a, o, p in zip(*(info[k].ravel() for k in ("demand", "ship", "acquisition", "order",
+                                                                          "profit")))]
         for i in range(n):
-            o = {ag: obs[i, k].copy() for k, ag in enumerate(self.agent_ids)}
-            r = ({ag: np.float64(rew[i, k]) for k, ag in enumerate(self.agent_ids)} if indep
-                 else {ag: np.float64(rew[i]) for ag in self.agent_ids})
+            b = i * N
+            o = dict(zip(ids, rows[b:b + N]))
+            r = dict(zip(ids, rv[b:b + N])) if indep else dict.fromkeys(ids, rv[i])
             if info is not None:
-                inf = {ag: {"period": period, "demand": info["demand"][i, k], "ship": info["ship"][i, k],
-                            "acquisition": info["acquisition"][i, k], "actual order": info["order"][i, k],
-                            "profit": info["profit"][i, k]} for k, ag in enumerate(self.agent_ids)}
+                inf = dict(zip(ids, infs[b:b + N]))
             else:
-                inf = {ag: {} for ag in self.agent_ids}
+                inf = {ag: {} for ag in ids}
             # RLlib's _MultiAgentEnvState.observe
             self._obs[i] = o
             lr = self._last_rew[i]
-            for ag, v in r.items():
-                lr[ag] = lr[ag] + v if (ag in lr and lr[ag] is not None) else v
+            if lr:
+                for ag, v in r.items():
+                    p = lr.get(ag)
+                    lr[ag] = v if p is None else p + v
+            else:
+                self._last_rew[i] = r
             ld = self._last_done[i]
-            for ag, v in {"__all__": done}.items():
-                ld[ag] = (ld[ag] or v) if ag in ld else v
+            ld["__all__"] = (ld["__all__"] or done) if "__all__" in ld else done
             self._last_info[i] = inf
             if done:
                 self._dones.add(i)

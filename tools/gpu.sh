@@ -17,6 +17,7 @@
 #   stamps:C:N       per-wave phase stamps of a diagnostic build (tools/stamp_probe.py)
 #   rehearse[:N]     bench.py --gpus N (default 2) --rehearse-one-gpu: every rank on GPU 0 with gloo, the
 #                    strong-scaled shards and the gather pass (plain, then --no-gather)
+#   pytest:FILES     the GPU tests of the given test files (comma-separated)
 #   py:SCRIPT[:ARGS] any python tool, ARGS comma-separated (its stdout to OUT/<script>.log)
 #   floors:R         interleaved A/B (tools/ab_multi.sh, R rounds) of the production step kernel and its
 #                    access-shape floor (IMENV_ABLATE=63: the same vector loads and stores, no
@@ -44,6 +45,11 @@ for task in "$@"; do
         > "$OUT/pytest_gpu.log" 2>&1; rc=$?
       tail -n 3 "$OUT/pytest_gpu.log"
       [ $rc -le 1 ] || fail "tests_all rc=$rc" "$OUT/pytest_gpu.log" ;;
+    pytest)
+      f=${a//,/ }
+      timeout -k 10 600 python -u -m pytest $f -m gpu -x -q --timeout 120 --timeout-method thread \
+        > "$OUT/pytest_sel.log" 2>&1 || fail "pytest $f" "$OUT/pytest_sel.log"
+      tail -n 1 "$OUT/pytest_sel.log" ;;
     smoke)
       timeout -k 10 180 python __graft_entry__.py smoke > "$OUT/smoke.log" 2>&1 || fail smoke "$OUT/smoke.log"
       echo "smoke ok" ;;
