@@ -346,6 +346,9 @@ def main():
     # rehearsal of the multi-rank path on a one-GPU box: every rank on device 0, gloo for the
     # barrier / max-reduction (the driver's N-GPU runs use one GPU per rank and RCCL)
     ap.add_argument("--rehearse-one-gpu", action="store_true", help=argparse.SUPPRESS)
+    # the RCCL path of an N-rank line at world size 1 on one GPU: a one-rank "nccl" process group, the
+    # census, barriers and max-reductions through it and the gather pass over RCCL (validation only)
+    ap.add_argument("--rccl-solo", action="store_true", help=argparse.SUPPRESS)
     # launcher / rendezvous / census path only, no GPU work (CPU tests)
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
     argv = sys.argv[1:]
@@ -375,7 +378,11 @@ def main():
         else:
             cpu = cpu_baseline(args.cpu_seconds, args.config)          # before the GPU is initialised
 
-    gather_on = gather_is_on(args, world) and world > 1
+    if args.rccl_solo and (world != 1 or args.rehearse_one_gpu):
+        sys.stderr.write("bench.py: --rccl-solo is the one-rank RCCL check (world size 1, no rehearsal)\n")
+        sys.exit(2)
+    dist_on = world > 1 or args.rccl_solo     # a process group (and its collectives) in this run
+    gather_on = (gather_is_on(args, world) and world > 1) or (args.rccl_solo and args.gather is not False)
     if gather_on and not args.rehearse_one_gpu:
         # RCCL records start / end events around every collective on its own stream (Work._get_duration)
         os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")
@@ -389,10 +396,14 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if dist_on:
         if args.rehearse_one_gpu:
             dist.init_process_group("gloo")
         else:
+            if args.rccl_solo:
+                for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", str(_free_port())), ("RANK", "0"),
+                             ("WORLD_SIZE", "1")):
+                    os.environ.setdefault(k, v)
             dist.init_process_group("nccl", device_id=dev)
     census = ranks_census(dist, dev)
     ranks_seen = len({c["rank"] for c in census})
@@ -516,19 +527,19 @@ def main():
         """The driver's timed region: barrier + synchronise, then body(), then synchronise; the wall time
         is read before the trailing barrier (every rank's own K steps, not the slowest rank's barrier
         exit), and the max over ranks is taken afterwards."""
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         out = body()
         torch.cuda.synchronize(dev)
         el = time.perf_counter() - t0
-        if world > 1:
+        if dist_on:
             dist.barrier()
         return el, out
 
     def max_over_ranks(*xs):
-        if world == 1:
+        if not dist_on:
             return xs
         tt = torch.tensor(list(xs), dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -724,6 +735,8 @@ def main():
         "gather": gather_info,
         "cpu_baseline": cpu,
     }
+    if args.rccl_solo:
+        out["rccl_solo"] = "one-rank nccl (RCCL) process group: census, barriers, max-reductions and the gather pass through RCCL"
     if kinfo.startswith("jit-diag:"):
         out["diagnostic_build"] = True
         out["roofline"]["traffic"] = None
@@ -732,7 +745,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     env.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

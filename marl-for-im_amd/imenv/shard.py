@@ -66,6 +66,12 @@ class PackedGather:
         self._work = [None] * buffers
         self._into = dist.get_backend(group) == "nccl"
         self._kept = None       # completed collectives, kept for timing (keep_works)
+        # the field views of every buffer, made once: a per-step loop then pays no torch view ops
+        # (about a dozen per step otherwise, each a few microseconds of host time)
+        self._send_views = [[self._field(b, j) for j in range(len(self.fields))] for b in self._send]
+        self._recv_views = [[self._field(b, j, lead=(self.world,)) for j in range(len(self.fields))]
+                            for b in self._recv]
+        self._recv_lists = [list(b.chunk(self.world)) for b in self._recv]
 
     def _field(self, buf, j, lead=()):
         shape, dtype = self.fields[j]
@@ -77,10 +83,10 @@ class PackedGather:
         return rows.view(dtype).view((self.world,) + shape)
 
     def send(self, k=0):
-        return [self._field(self._send[k], j) for j in range(len(self.fields))]
+        return list(self._send_views[k])
 
     def gathered(self, k=0):
-        return [self._field(self._recv[k], j, lead=(self.world,)) for j in range(len(self.fields))]
+        return list(self._recv_views[k])
 
     def start(self, k=0):
         """Launch the all-gather of send buffer k (async: RCCL's stream waits for the work already
@@ -90,8 +96,7 @@ class PackedGather:
             self._work[k] = dist.all_gather_into_tensor(self._recv[k], self._send[k], group=self.group,
                                                         async_op=True)
         else:
-            self._work[k] = dist.all_gather(list(self._recv[k].chunk(self.world)), self._send[k], group=self.group,
-                                            async_op=True)
+            self._work[k] = dist.all_gather(self._recv_lists[k], self._send[k], group=self.group, async_op=True)
 
     def wait(self, k=0):
         w = self._work[k]
@@ -129,23 +134,32 @@ class StepGather(PackedGather):
         super().__init__([(obs_like.shape, obs_like.dtype), (reward_like.shape, reward_like.dtype)],
                          obs_like.device, group, buffers)
         self.nbuf = buffers
+        # result()'s [world * n, ...] tensors: cached where flatten is a view of the receive buffer
+        # (world 1), made per call where it is a copy (world > 1: the ranks' rows sit a packed chunk apart)
+        self._flat = []
+        for views in self._recv_views:
+            f = tuple(v.flatten(0, 1) for v in views)
+            self._flat.append(f if all(a.data_ptr() == v.data_ptr() for a, v in zip(f, views)) else None)
 
     def obs_out(self, t):
         """Send view for step t's obs. Orders the current stream after the collective that last read
         this buffer (step t - nbuf), so the env cannot overwrite it while it is in flight."""
         self.wait(t % self.nbuf)
-        return self.send(t % self.nbuf)[0]
+        return self._send_views[t % self.nbuf][0]
 
     def reward_out(self, t):
         self.wait(t % self.nbuf)
-        return self.send(t % self.nbuf)[1]
+        return self._send_views[t % self.nbuf][1]
 
     def start(self, t=0):
         super().start(t % self.nbuf)
 
     def result(self, t):
         self.wait(t % self.nbuf)
-        o, r = self.gathered(t % self.nbuf)
+        f = self._flat[t % self.nbuf]
+        if f is not None:
+            return f
+        o, r = self._recv_views[t % self.nbuf]
         return o.flatten(0, 1), r.flatten(0, 1)
 
     def __call__(self, obs, reward):
