@@ -334,6 +334,9 @@ class InvMultiAgentBaseEnv(_BaseEnv):
     def get_sub_environments(self):
         return []
 
+    def try_render(self, env_id=None):
+        return None
+
     def stop(self):
         self._b.close()
 
