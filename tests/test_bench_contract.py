@@ -163,3 +163,12 @@ def test_a_failing_rank_fails_the_launch():
 def test_steps_must_be_positive():
     r = _run_rc(["--steps", "0", "--no-cpu-baseline"], timeout=60)
     assert r.returncode == 2 and "--steps must be >= 1" in r.stderr
+
+
+def test_rccl_solo_is_world_size_one_only():
+    """--rccl-solo is the one-rank RCCL check: refused with a rehearsal or under a multi-rank launcher."""
+    r = _run_rc(["--rccl-solo", "--rehearse-one-gpu", "--no-cpu-baseline"], timeout=60)
+    assert r.returncode == 2 and "--rccl-solo" in r.stderr
+    r = _run_rc(["--gpus", "2", "--rccl-solo", "--no-cpu-baseline"], timeout=60, WORLD_SIZE="2", RANK="0",
+                LOCAL_RANK="0")
+    assert r.returncode == 2 and "--rccl-solo" in r.stderr
