@@ -1,0 +1,88 @@
+"""Handles past every 32-bit offset boundary, exact against the oracle on slices that straddle them.
+
+imenv_create accepts up to 2^31 envs per handle (include/imenv.h). These runs use handles large
+enough that the step kernel's element offsets pass 2^31 and its byte offsets pass 2^32. That holds for
+observations, actions and (C2) rewards. A 32-bit index anywhere on those paths would put the envs
+past the boundary on the wrong rows. C2 runs 2^29 + 4,096 envs (about 47 GB in all) and 2^31 (the
+ABI's maximum, about 210 GB). C4 (the tree, with history observations) runs 2^28 + 4,096 (about 45
+GB). For each boundary, a 256-env slice that straddles it is checked over a whole episode against the
+oracle under the same Philox keys. In-kernel demand, float32 actions; the JIT and the ahead-of-time
+kernels both run.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle.im_oracle import OracleEnv
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+C2 = dict(num_stages=4, num_periods=30, init_inv=np.ones(4) * 10, inv_target=np.zeros(4),
+          inv_max=np.ones(4) * 30, price=np.array([5, 4, 3, 2, 1]),
+          stock_cost=np.array([0.35, 0.3, 0.4, 0.2]), backlog_cost=np.array([0.5, 0.7, 0.6, 0.9]),
+          delay=np.array([1, 2, 3, 1]), demand_dist="poisson", mu=5, seed=52, independent=False)
+C4 = dict(num_nodes=4, connections={0: [1], 1: [2, 3], 2: [], 3: []}, num_periods=30,
+          init_inv=np.ones(4) * 10, inv_target=np.zeros(4), inv_max=np.ones(4) * 30,
+          stock_cost=np.array([0.35, 0.3, 0.4, 0.4]), backlog_cost=np.array([0.5, 0.7, 0.6, 0.6]),
+          delay=np.array([1, 2, 1, 1]), demand_dist="poisson", mu=5, seed=52, time_dependency=True,
+          prev_demand=True, independent=False)
+
+
+def boundary_slices(n, row_bytes, act_bytes=16, rew_bytes=8, width=256):
+    """Slices of `width` envs around every env whose observation / action / reward element or byte
+    offset first reaches 2^31 or 2^32, plus both ends of the batch."""
+    starts = {0, n - width}
+    for per_env in (row_bytes, act_bytes, rew_bytes):
+        for elem in (4, 8):
+            if per_env % elem:
+                continue
+            for lim in (1 << 31, 1 << 32):
+                for unit in (elem, 1):          # element index, byte offset
+                    e = -(-lim * unit // per_env)  # first env at or past the boundary
+                    if 0 < e < n:
+                        starts.add(min(max(e - width // 2, 0), n - width))
+    return sorted(starts)
+
+
+@pytest.mark.parametrize("kind,cfg,n,mode", [
+    ("MAIM", C2, (1 << 29) + 4096, "jit"), ("MAIM", C2, (1 << 29) + 4096, "aot"),
+    ("MAIM_div", C4, (1 << 28) + 4096, "jit"), ("MAIM_div", C4, (1 << 28) + 4096, "aot"),
+    ("MAIM", C2, 1 << 31, "jit")])         # the largest handle imenv_create accepts (about 210 GB here)
+def test_offsets_past_32_bits_match_oracle(kind, cfg, n, mode):
+    from imenv import VectorInvEnv
+    free, _ = torch.cuda.mem_get_info(DEV)
+    env = VectorInvEnv(kind, cfg, n_envs=n, device=DEV)
+    env.set_jit(1 if mode == "jit" else 0)
+    N, F = env.N, env.F
+    need = n * (N * 4 + N * F * 4 + 8 + 32)      # actions, observations, rewards, state + error flags
+    if free < 1.1 * need:
+        env.close()
+        pytest.skip("needs %.0f GB of free device memory, %.0f GB free" % (need / 2**30, free / 2**30))
+    obs = torch.empty((n, N, F), dtype=torch.float32, device=DEV)
+    rew = torch.empty(env.reward_shape(), dtype=torch.float64, device=DEV)
+    act = torch.empty((n, N), dtype=torch.float32, device=DEV)
+    starts = boundary_slices(n, N * F * 4, act_bytes=N * 4, rew_bytes=rew[0].numel() * 8)
+    assert len(starts) >= 4
+    k = 256
+    oras = [OracleEnv(kind, cfg, n_envs=k) for _ in starts]
+    env.reset(obs_out=obs)
+    for s, ora in zip(starts, oras):
+        r0 = ora.reset(rng=dict(seed=52, episode=0, env_offset=s, dist="poisson", mu=5))
+        np.testing.assert_array_equal(obs[s:s + k].cpu().numpy(), r0.astype(np.float32), err_msg="reset @%d" % s)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(11)
+    for t in range(30):
+        torch.rand((n, N), generator=g, device=DEV, out=act)
+        act.mul_(2.2).sub_(1.1)
+        env.step(act, obs_out=obs, reward_out=rew)
+        for s, ora in zip(starts, oras):
+            o_c, r_c, _, _ = ora.step(act[s:s + k].double().cpu().numpy())
+            np.testing.assert_array_equal(obs[s:s + k].cpu().numpy(), o_c.astype(np.float32),
+                                          err_msg="%s obs t=%d @%d" % (kind, t, s))
+            np.testing.assert_array_equal(rew[s:s + k].cpu().numpy(), r_c, err_msg="%s reward t=%d @%d" % (kind, t, s))
+    flags, anyv = env.errors()
+    assert anyv == 0
+    env.close()
+    del obs, rew, act
+    torch.cuda.empty_cache()
