@@ -86,3 +86,70 @@ def test_offsets_past_32_bits_match_oracle(kind, cfg, n, mode):
     env.close()
     del obs, rew, act
     torch.cuda.empty_cache()
+
+
+def _free_bytes():
+    torch.cuda.empty_cache()
+    return torch.cuda.mem_get_info(DEV)[0]
+
+
+@pytest.mark.parametrize("kind,base", [("IM", "serial4"), ("IM_div", "div1")])
+def test_plan_replay_offsets_past_32_bits(kind, base):
+    """Plan replay with one float64 plan per scenario over 2^25 + 256 scenarios. The plans' element
+    offsets pass 2^31 and their byte offsets 2^32 from period 4 on; the per-step reward rows pass 2^32
+    bytes too. Scenario slices across the batch are checked against the oracle's replay under the
+    same keys. The plans are made on the device, already in the kernel's [T][P][S][N] layout, and
+    handed over as a [P][S][T][N] view, so no transposed copy is made."""
+    import gen_cfg
+    from oracle import plan as pl
+    from imenv.plan import PlanRollout
+    cfg = gen_cfg.__dict__[base](standardise_state=False, standardise_actions=False)
+    N, T, S = cfg.get("num_stages", cfg.get("num_nodes")), cfg.get("num_periods", 30), (1 << 25) + 256
+    need = S * (T * N * 8 + T * 8 + 5 * 8) + (1 << 30)
+    if _free_bytes() < 1.1 * need:
+        pytest.skip("needs %.0f GB of free device memory" % (need / 2**30))
+    g = torch.Generator(device=DEV)
+    g.manual_seed(4)
+    x = torch.randint(0, 25, (T, 1, S, N), generator=g, device=DEV).to(torch.float64)
+    x += 0.5 * torch.randint(0, 2, (T, 1, S, N), generator=g, device=DEV)
+    pr = PlanRollout(kind, cfg, device=DEV)
+    out = pr.run(x.permute(1, 2, 0, 3), per_episode=True, n_scenarios=S, episode=1)
+    for s in (0, S // 3, S // 2 + 77, S - 256):
+        k = 256
+        rng = dict(seed=cfg["seed"], episode=1, env_offset=s, dist="poisson", mu=cfg.get("mu", 5))
+        ref = pl.plan_rollout(kind, cfg, x[:, :, s:s + k].cpu().numpy(), per_episode=True, n_scenarios=k, rng=rng)
+        for name in ("return", "inventory", "backlog", "customer_backlog"):
+            np.testing.assert_array_equal(out[name][:, s:s + k].cpu().numpy(), ref[name], err_msg="%s @%d" % (name, s))
+        np.testing.assert_array_equal(out["rewards"][:, s:s + k].cpu().numpy(), np.transpose(ref["rewards"], (1, 2, 0)),
+                                      err_msg="rewards @%d" % s)
+    pr.close()
+    del x, out
+    torch.cuda.empty_cache()
+
+
+def test_base_stock_rollout_offsets_past_32_bits():
+    """128 base-stock policies x (2^22 + 64) drawn scenarios in one launch (1.6e10 env-steps): the
+    per-episode output rows ([stat][P][S] float64) pass 2^31 elements and 2^32 bytes. (policy,
+    scenario) slices across the batch equal the oracle's rollout under the same keys."""
+    import gen_cfg
+    from scipy.stats import poisson
+    from oracle import base_stock as bs
+    from imenv.policy import BaseStockRollout
+    cfg = gen_cfg.serial4(standardise_state=False, standardise_actions=False)
+    P, S = 128, (1 << 22) + 64
+    need = 5 * P * S * 8 + (1 << 30)
+    if _free_bytes() < 1.1 * need:
+        pytest.skip("needs %.0f GB of free device memory" % (need / 2**30))
+    pol = np.random.RandomState(9).uniform(0, 50, size=(P, 4))
+    ro = BaseStockRollout("IM", cfg, device=DEV)
+    out = ro.run(pol, n_scenarios=S, episode=6)
+    for p, s in ((0, 0), (127, S - 200), (64, S // 2), (100, 12345), (31, S - 4000)):
+        k = 200
+        rng = dict(seed=cfg["seed"], episode=6, env_offset=s, dist="poisson", mu=5)
+        ref = bs.rollout("IM", cfg, pol[p:p + 1], n_scenarios=k, rng=rng, pmf=lambda v: poisson.pmf(v, mu=5))
+        for name in ("return", "objective", "inventory", "backlog", "customer_backlog"):
+            np.testing.assert_array_equal(out[name][p, s:s + k].cpu().numpy(), ref[name][0],
+                                          err_msg="%s (%d, %d)" % (name, p, s))
+    ro.close()
+    del out
+    torch.cuda.empty_cache()
