@@ -153,3 +153,45 @@ def test_base_stock_rollout_offsets_past_32_bits():
     ro.close()
     del out
     torch.cuda.empty_cache()
+
+
+def test_gae_and_cc_observation_offsets_past_32_bits():
+    """GAE over a [30, 2^27 + 64] buffer (4.0e9 elements per row array) and centralised-critic rows
+    for [2^26 + 64] envs x 4 agents (4.0e9 output elements): sampled envs at the start, across the
+    2^31-element boundaries and at the end equal the oracle restatements."""
+    from oracle.gae import gae_batch
+    from oracle.cc_obs import cc_observation as cc_ref
+    from imenv.rollout import gae
+    from imenv.critic import cc_observation
+    T, n = 30, (1 << 27) + 64
+    need = T * n * (8 + 4 + 4 + 4) + (1 << 30)
+    if _free_bytes() < 1.1 * need:
+        pytest.skip("needs %.0f GB of free device memory" % (need / 2**30))
+    g = torch.Generator(device=DEV)
+    g.manual_seed(12)
+    r = torch.randn((T, n), generator=g, device=DEV, dtype=torch.float64) * 30
+    v = torch.randn((T, n), generator=g, device=DEV) * 100
+    adv, vt = gae(r, v)
+    cols = np.unique(np.concatenate([np.arange(0, 64), np.arange(n - 64, n),
+                                     np.arange(-64, 64) + (1 << 31) // T, np.arange(-64, 64) + (1 << 32) // (4 * T),
+                                     np.random.RandomState(1).randint(0, n, 256)]))
+    idx = torch.as_tensor(cols, device=DEV)
+    ea, ev = gae_batch(r[:, idx].cpu().numpy(), v[:, idx].cpu().numpy())
+    np.testing.assert_array_equal(adv[:, idx].cpu().numpy(), ea)
+    np.testing.assert_array_equal(vt[:, idx].cpu().numpy(), ev)
+    del r, v, adv, vt
+    torch.cuda.empty_cache()
+
+    m = (1 << 26) + 64                    # CC rows: [m, 4, 15] float32 = 4.0e9 elements
+    obs = torch.rand((m, 4, 3), generator=g, device=DEV) * 2 - 1
+    act = torch.rand((m, 4), generator=g, device=DEV) * 3 - 1.5
+    got = cc_observation(obs, act)
+    assert got.shape == (m, 4, 15)
+    rows = np.unique(np.concatenate([np.arange(0, 64), np.arange(m - 64, m),
+                                     np.arange(-64, 64) + (1 << 31) // 60, np.arange(-64, 64) + (1 << 32) // 240,
+                                     np.random.RandomState(2).randint(0, m, 256)]))
+    ri = torch.as_tensor(rows, device=DEV)
+    exp = cc_ref(obs[ri].cpu().numpy(), act[ri].cpu().numpy())
+    np.testing.assert_array_equal(got[ri].cpu().numpy(), exp)
+    del obs, act, got
+    torch.cuda.empty_cache()
