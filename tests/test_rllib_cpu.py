@@ -147,3 +147,23 @@ def test_oracle_episode_sequence_on_the_stand_in(cpu_batch, kind, cfg_name, monk
     import test_rllib_gpu as g
     monkeypatch.setattr(g, "DEV", "cpu")
     g.test_batched_surfaces_match_the_oracle_over_episodes(kind, cfg_name)
+
+
+@pytest.mark.parametrize("form", ["array1", "scalar", "list", "zero_d", "mixed"])
+def test_send_actions_accepts_rllib_action_forms(cpu_batch, form):
+    """An agent's action may come as a [1] array (Box(1) policies), a Python / NumPy scalar, a list or
+    a 0-d array, and a batch may mix them: the stepped values are the same."""
+    meta, d = load_case("C2_MAIM4")
+    E = meta["E"]
+    env = cpu_batch.InvMultiAgentBaseEnv(meta["kind"], meta["config"], num_envs=E, episode_inputs=_inputs(meta, d))
+    ids = env.agent_ids
+    env.poll()
+    a = d["actions"][:, 0]
+    conv = {"array1": lambda x, i: np.array([x]), "scalar": lambda x, i: float(x), "list": lambda x, i: [x],
+            "zero_d": lambda x, i: np.array(x),
+            "mixed": lambda x, i: (np.array([x]), np.float64(x), [x], np.array(x))[i % 4]}[form]
+    env.send_actions({i: {ag: conv(a[i, k], i + k) for k, ag in enumerate(ids)} for i in range(E)})
+    obs, rew, _, _, _ = env.poll()
+    for i in range(E):
+        np.testing.assert_array_equal(np.stack([obs[i][ag] for ag in ids]), d["obs"][i, 0])
+    env.stop()
