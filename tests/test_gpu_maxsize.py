@@ -51,7 +51,7 @@ def boundary_slices(n, row_bytes, act_bytes=16, rew_bytes=8, width=256):
     ("MAIM", C2, 1 << 31, "jit")])         # the largest handle imenv_create accepts (about 210 GB here)
 def test_offsets_past_32_bits_match_oracle(kind, cfg, n, mode):
     from imenv import VectorInvEnv
-    free, _ = torch.cuda.mem_get_info(DEV)
+    free = _free_bytes()
     env = VectorInvEnv(kind, cfg, n_envs=n, device=DEV)
     env.set_jit(1 if mode == "jit" else 0)
     N, F = env.N, env.F
@@ -194,4 +194,28 @@ def test_gae_and_cc_observation_offsets_past_32_bits():
     exp = cc_ref(obs[ri].cpu().numpy(), act[ri].cpu().numpy())
     np.testing.assert_array_equal(got[ri].cpu().numpy(), exp)
     del obs, act, got
+    torch.cuda.empty_cache()
+
+
+def test_column_stats_offsets_past_32_bits():
+    """The evaluation harness's column statistics (imenv_column_stats) over a (2^28 + 12,345) x 8
+    float64 matrix (2^31 + 98,760 elements, 17 GB): every column's mean and std equal a float64
+    torch reduction of the same matrix within 1e-10 relative (means also 1e-9 absolute)."""
+    from imenv import _native as nat
+    rows, cols = (1 << 28) + 12345, 8
+    if _free_bytes() < 1.2 * rows * cols * 8 + (1 << 30):
+        pytest.skip("needs %.0f GB of free device memory" % (rows * cols * 8 / 2**30))
+    g = torch.Generator(device=DEV)
+    g.manual_seed(13)
+    x = torch.randn((rows, cols), generator=g, dtype=torch.float64, device=DEV)
+    x.mul_(torch.arange(1, cols + 1, device=DEV, dtype=torch.float64) * 7).add_(torch.arange(cols, device=DEV) * 3.0)
+    x[-1] = 1e6                          # the last row (past the 2^31-element mark) must be counted
+    out = torch.empty((cols, 2), dtype=torch.float64, device=DEV)
+    nat.check(nat.load().imenv_column_stats(x.data_ptr(), rows, cols, out.data_ptr(), None), "column_stats")
+    torch.cuda.synchronize()
+    mean = x.mean(dim=0)
+    std = x.std(dim=0, correction=0)
+    np.testing.assert_allclose(out[:, 0].cpu().numpy(), mean.cpu().numpy(), rtol=1e-10, atol=1e-9)
+    np.testing.assert_allclose(out[:, 1].cpu().numpy(), std.cpu().numpy(), rtol=1e-10)
+    del x
     torch.cuda.empty_cache()
