@@ -142,8 +142,11 @@ class _Batch:
         info = None
         if self.info:
             iv = lambda j: hi[j * n * N:(j + 1) * n * N].reshape(n, N).astype(np.float64)
+            # profit is copied out of the host mirror like the others (astype copies): the mirror is
+            # rewritten by the next step, and RLlib keeps infos in its sample batches (IM_env.py:350
+            # hands out a fresh array per step)
             info = dict(order=iv(0), demand=iv(1), acquisition=iv(2), ship=iv(3),
-                        profit=hf[n * N * F + n * self.nr:].reshape(n, N))
+                        profit=hf[n * N * F + n * self.nr:].reshape(n, N).copy())
         return obs, rew, info, t
 
     def close(self):
@@ -263,6 +266,7 @@ class InvMultiAgentBaseEnv(_BaseEnv):
                 rew, done, info = lr, ld, li
                 done["__all__"] = False
                 self._last_rew[i], self._last_done[i], self._last_info[i] = {}, {}, {}
+                self._obs[i] = {}            # released once: a second poll before send_actions gets none
             else:
                 rew, done, info = {}, {"__all__": False}, {}
             self._last_done[i]["__all__"] = False

@@ -167,3 +167,47 @@ def test_send_actions_accepts_rllib_action_forms(cpu_batch, form):
     for i in range(E):
         np.testing.assert_array_equal(np.stack([obs[i][ag] for ag in ids]), d["obs"][i, 0])
     env.stop()
+
+
+def test_infos_outlive_the_next_step(cpu_batch):
+    """Infos handed out by one vector_step keep their values after the next one (RLlib stores them in its
+    sample batches): every array in them is a copy, not a view of the host mirror the next step rewrites
+    (IM_env.py:350 builds a fresh info dict per step)."""
+    meta, d = load_case("C1_IM4")
+    E = meta["E"]
+    env = cpu_batch.InvVectorEnv(meta["kind"], meta["config"], num_envs=E, episode_inputs=_inputs(meta, d))
+    env.vector_reset()
+    _, _, _, infos0 = env.vector_step([d["actions"][i, 0] for i in range(E)])
+    env.vector_step([d["actions"][i, 1] for i in range(E)])
+    for k in ("demand", "ship", "acquisition", "profit"):
+        np.testing.assert_array_equal(np.stack([inf[k] for inf in infos0]), d[k][:, 0], err_msg=k)
+    ma_meta, md = load_case("C2_MAIM4")
+    ma = cpu_batch.InvMultiAgentBaseEnv(ma_meta["kind"], ma_meta["config"], num_envs=ma_meta["E"],
+                                        episode_inputs=_inputs(ma_meta, md))
+    ids = ma.agent_ids
+    ma.poll()
+    ma.send_actions({i: {ag: np.array([md["actions"][i, 0, k]]) for k, ag in enumerate(ids)} for i in range(ma_meta["E"])})
+    _, _, _, inf0, _ = ma.poll()
+    ma.send_actions({i: {ag: np.array([md["actions"][i, 1, k]]) for k, ag in enumerate(ids)} for i in range(ma_meta["E"])})
+    ma.poll()
+    for i in range(ma_meta["E"]):
+        for k, ag in enumerate(ids):
+            assert inf0[i][ag]["profit"] == md["profit"][i, 0, k]
+
+
+def test_second_poll_releases_nothing_new(cpu_batch):
+    """A poll with no send_actions since the previous one hands out no observation again (RLlib's
+    _MultiAgentEnvState releases an observation once)."""
+    meta, d = load_case("C2_MAIM4")
+    E = meta["E"]
+    env = cpu_batch.InvMultiAgentBaseEnv(meta["kind"], meta["config"], num_envs=E, episode_inputs=_inputs(meta, d))
+    ids = env.agent_ids
+    env.poll()
+    obs, _, _, _, _ = env.poll()
+    assert all(obs[i] == {} for i in range(E))
+    env.send_actions({i: {ag: np.array([d["actions"][i, 0, k]]) for k, ag in enumerate(ids)} for i in range(E)})
+    obs, rew, _, _, _ = env.poll()
+    assert all(sorted(obs[i]) == sorted(ids) for i in range(E))
+    obs, rew, dones, _, _ = env.poll()
+    assert all(obs[i] == {} and rew[i] == {} and dones[i] == {"__all__": False} for i in range(E))
+    env.stop()
