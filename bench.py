@@ -249,6 +249,20 @@ def shard_plan(scaling, config, n_envs, world, rank):
     return weak_offset(total, rank), total, total * world
 
 
+def episode_phase(W, K, T):
+    """Period of the bench's step 0: step s runs period (s + phase) mod T. With K >= T every window of K
+    steps holds a reset anyway (phase 0). A shorter window (the driver's --steps 20 --warmup 5) is placed so
+    that the episode boundary falls in its middle: the timed steps then include a reset kernel, as they do
+    on average in a long run (the reset runs every 30 steps inside the timed loop). The
+    handle is brought to that period by untimed steps before the warmup."""
+    return 0 if K >= T else (-(W + K // 2)) % T
+
+
+def resets_in_window(W, K, T, phase):
+    """Reset kernels inside the timed steps W .. W+K-1 (one before each period-0 step)."""
+    return sum(1 for s in range(W, W + K) if (s + phase) % T == 0)
+
+
 def gather_is_on(args, world):
     """The per-step all-gather leg: explicit --gather / --no-gather, else on whenever there is more than
     one rank (C5: the obs / reward batch gathered over xGMI)."""
@@ -444,7 +458,7 @@ def main():
     obs64 = {}     # float64 observation buffers of the informational alt_obs_f64 leg (made on demand)
 
     def run(first, steps, events=None, gather=None, f64=False):
-        """Steps first .. first+steps-1 of the bench's step sequence (period t = step mod T). With a
+        """Steps first .. first+steps-1 of the bench's step sequence (period t = (step + phase) mod T). With a
         StepGather the env writes into its send buffers and step s's all-gather runs under step s+1;
         with f64 the observations are float64 (the reference's dtype). Returns the number of resets it
         ran."""
@@ -452,7 +466,7 @@ def main():
         resets = 0
         op, od = (obs64["ptr"], nat.F64) if f64 else (o_ptr, nat.F32)
         for s in range(first, first + steps):
-            t = s % T
+            t = (s + phase) % T
             if t == 0:
                 reset(sptr)
                 resets += 1
@@ -493,7 +507,8 @@ def main():
         falls behind over the K steps lets the launches queue up, so the events time them back to back;
         the wall-clock value is unchanged up to the 5% margin on that spin (the host paces the loop
         either way: the last launch still follows the host's last enqueue). When the host keeps
-        ahead (the metric's 2^20-env launches), no spin. Calibrated on two untimed episodes (the step
+        well ahead (the metric's 2^20-env launches), no spin; when it keeps ahead by a thin margin, a
+        short fixed lead (below). Calibrated on two untimed episodes (the step
         sequence stays aligned: 2T steps bring the handle back to the same period). Returns (cycles,
         host us per step, GPU us per step)."""
         if not hasattr(torch.cuda, "_sleep"):    # (a private torch helper: without it, no pacing)
@@ -517,9 +532,14 @@ def main():
         e1.record(stream)
         e1.synchronize()
         g = e0.elapsed_time(e1) * 1e3 / n_cal
-        if h <= g:
-            return 0, h, g
-        return int(K * (h - g) * 1.05 / us_per_cycle), h, g
+        if h > g:
+            return int(K * (h - g) * 1.05 / us_per_cycle), h, g
+        if h > 0.6 * g:
+            # the host keeps ahead, but by less than 40% of a launch: one late enqueue (a scheduler or
+            # allocator hiccup of tens of us) would leave the GPU idle inside an event pair. A fixed lead
+            # of min(10% of the K launches, 50 us) absorbs it; the wall clock pays that lead in full
+            return int(min(0.1 * K * g, 50.0) / us_per_cycle), h, g
+        return 0, h, g
 
     spin_info = {}
 
@@ -545,14 +565,19 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         return tuple(v.item() for v in tt)
 
-    def timed(W, K, f64=False):
-        """W untimed warmup steps (the first one resets), then exactly K timed steps of the same step
-        sequence, so the timed region holds the resets at its episode boundaries. No collective. Returns
-        (wall s, kernel ms per launch, algorithmic bytes per timed launch, timed launches, resets timed),
-        max over ranks."""
+    def warm(W, **kw):
+        """Bring the handle to step W of the sequence: a reset and the untimed steps of periods 0 ..
+        phase - 1 (episode_phase), then the W warmup steps."""
         if W == 0:
-            run(0, 1, f64=f64)     # no warmup asked for: one step outside the sequence builds the hipRTC kernel
-        run(0, W, f64=f64)
+            run(-phase, 1, **kw)     # no warmup asked for: one step outside the sequence builds the hipRTC kernel
+        run(-phase, phase + W, **kw)
+
+    def timed(W, K, f64=False):
+        """W untimed warmup steps, then exactly K timed steps of the same step sequence, so the timed
+        region holds the resets at its episode boundaries (at least one: episode_phase). No collective.
+        Returns (wall s, kernel ms per launch, algorithmic bytes per timed launch, timed launches, resets
+        timed), max over ranks."""
+        warm(W, f64=f64)
         spin, h_us, g_us = lead_spin(W, K, f64)
         if not spin_info:      # the line's own timed region (not the informational alt-store run)
             spin_info.update(host_us_per_step=None if h_us != h_us else round(h_us, 3),
@@ -582,18 +607,39 @@ def main():
         """The same W + K step sequence with C5's per-step all-gather pipelined under the next step (a
         second pass after the line's own): the wall time of the K steps including every collective, max
         over ranks."""
-        run(0, max(W, 1), gather=gather)
+        warm(W, gather=gather)
         gather.keep_works(True)
         el, _ = bracket(lambda: run(W, K, gather=gather))
         return max_over_ranks(el)[0]
 
     pool = []
     W, K = args.warmup, args.steps
+    phase = episode_phase(W, K, T)
     env.set_store_policy(args.store)
     el, kern_ms, bytes_per_launch, launches, resets_timed = timed(W, K)
     kinfo = env.kernel_info()          # the timed kernel (before the informational runs below)
 
+    # the reset kernel alone (informational; the line's value already holds resets_timed of them): R
+    # back-to-back resets queued behind a busy-wait, HIP events on the kernel's stream
+    reset_us = None
+    if hasattr(torch.cuda, "_sleep"):
+        torch.cuda.synchronize(dev)
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(2000000)
+        r0.record(stream)
+        for _ in range(20):
+            reset(sptr)
+        r1.record(stream)
+        r1.synchronize()
+        reset_us = r0.elapsed_time(r1) * 1e3 / 20
+
     gather_info = None
+    if gather_on and args.scaling == "strong" and global_envs % world:
+        # all_gather_into_tensor needs one send size on every rank; uneven shards would hand RCCL
+        # different counts (undefined behaviour: a hang or a corrupt buffer, not an exception)
+        gather_on = False
+        gather_info = {"skipped": "%d envs do not split evenly over %d ranks: the all-gather needs equal shards"
+                                  % (global_envs, world)}
     if gather_on:
         backend = dist.get_backend()
         try:
@@ -604,7 +650,24 @@ def main():
                                "%s (RCCL over xGMI)" % backend if backend == "nccl" else backend,
                                pipelined_value=round(global_envs * K / g_el, 1),
                                pipelined_ms_per_step=round(g_el / K * 1e3, 6),
-                               pipelined_over_gather_free=round(el / g_el, 4))
+                               pipelined_over_gather_free=round(el / g_el, 4),
+                               pipelined_form="eager: one host launch per step and per collective")
+            if backend == "nccl":
+                # the same pipeline with the host out of the loop: one episode's reset, T steps and T
+                # all-gathers captured into one HIP graph and replayed
+                try:
+                    gg = graph_gather_run(torch, dist, dev, gth, reset, lib, nat, a_ptr, T, h)
+                    gather_info["graph"] = gg
+                    if gg["ms_per_step"] * 1e-3 < g_el / K:
+                        gather_info["eager"] = {k: gather_info[k] for k in ("pipelined_value", "pipelined_ms_per_step",
+                                                                             "pipelined_over_gather_free")}
+                        gather_info.update(pipelined_value=round(global_envs / (gg["ms_per_step"] * 1e-3), 1),
+                                           pipelined_ms_per_step=gg["ms_per_step"],
+                                           pipelined_over_gather_free=round(el / K / (gg["ms_per_step"] * 1e-3), 4),
+                                           pipelined_form="HIP graph: reset + %d steps + %d all-gathers per replay "
+                                                          "(gather.graph), the eager form under gather.eager" % (T, T))
+                except Exception as ex:
+                    gather_info["graph"] = {"error": "%s: %s" % (type(ex).__name__, str(ex)[:300])}
             del gth
         except Exception as ex:          # informational leg: the line still reports the gather-free pass
             gather_info = {"error": "%s: %s" % (type(ex).__name__, str(ex)[:300])}
@@ -698,13 +761,17 @@ def main():
         "gpus_seen": gpus_seen if not args.rehearse_one_gpu else 1,
         "launcher": launcher,
         "resets_timed": resets_timed,
+        "value_basis": "the gather-free pass (env steps incl. their resets; the per-step all-gather of C5 is "
+                       "timed in a second pass: gather.pipelined_value)" if gather_on else
+                       "env steps incl. the resets inside the timed region; no collective",
         "config": {
             "workload": "%s%s: %s, %s, 30-period episodes; %d timed steps, %d of them "
-                        "preceded by the episode's reset kernel inside the timed region"
+                        "preceded by the episode's reset kernel inside the timed region (step s runs period "
+                        "(s + %d) mod 30)"
                         % (args.config, " at the metric's size" if args.config == "C2" and global_envs == 1 << 20
-                           else "", cdesc, shards, K, resets_timed),
+                           else "", cdesc, shards, K, resets_timed, phase),
             "n_envs_per_gpu": n, "global_envs": global_envs, "env_offset": env_off, "num_stages": N,
-            "obs_features": F, "num_periods": T,
+            "obs_features": F, "num_periods": T, "episode_phase": phase,
             "parallelism": "env-sharded x%d (one process per GPU%s, no data-path collective in the timed pass%s)"
                            % (world, ", all on GPU 0 with gloo: rehearsal" if args.rehearse_one_gpu else "",
                               "; the per-step all-gather of obs/reward timed in a second pass (\"gather\")"
@@ -721,6 +788,7 @@ def main():
             "kernel": kinfo,
             "kernel_us": round(kern_ms * 1e3, 3),
             "kernel_samples": launches,
+            "reset_us": round(reset_us, 3) if reset_us is not None else None,
             "bytes_per_env_step": round(bytes_per_launch / n, 3),
             "bytes_per_env_step_steady": b_steady,
             "bytes_per_env_step_episode_avg": round(b_avg, 3),
@@ -797,10 +865,81 @@ def gather_report(gather, dist, dev, stream, K, world, n):
         "gather_us": round(in_loop_max * 1e3, 3) if in_loop_max is not None else None,
         "gather_us_source": "collective-stream events per pipelined collective (max over ranks of the mean)"
                             if in_loop_max is not None else "unavailable (backend records no per-collective times)",
+        "recv_gbs": round(recv / (in_loop_max * 1e-3) / 1e9, 1) if in_loop_max else None,
         "gather_alone_us": round(t[1].item() * 1e3, 3),
         "gather_alone_recv_gbs": round(recv / (t[1].item() * 1e-3) / 1e9, 1),
         "collectives_timed": len(works),
     }
+
+
+def graph_gather_run(torch, dist, dev, gather, reset, lib, nat, a_ptr, T, h, replays=10):
+    """C5's per-step all-gather with the host out of the loop: one episode (reset, T steps into the
+    StepGather's double-buffered send views, each step's all_gather_into_tensor started on the
+    collective's stream under the next step) captured into one HIP graph and replayed back to back.
+    Also T collectives alone in a graph of their own (the collective's device time without the
+    host's launch pacing). RCCL only (gloo collectives run on the host)."""
+    world = dist.get_world_size()
+    torch.cuda.synchronize(dev)
+    gather.wait(0)
+    gather.wait(1)
+    gather.keep_works(False)          # no Work objects are kept for captured collectives
+    s = torch.cuda.Stream(dev)
+    g = torch.cuda.CUDAGraph()
+    dist.barrier()
+    with torch.cuda.graph(g, stream=s):
+        sp = torch.cuda.current_stream(dev).cuda_stream
+        for t in range(T):
+            if t == 0:
+                reset(sp)
+            rc = lib.imenv_step(h, a_ptr[t], nat.F32, gather.obs_out(t).data_ptr(), nat.F32,
+                                gather.reward_out(t).data_ptr(), None, None, sp)
+            if rc:
+                nat.check(rc, "imenv_step")
+            gather.start(t)
+            if t > 0:
+                gather.result(t - 1)
+        gather.result(T - 1)
+    cur = torch.cuda.current_stream(dev)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(cur)
+    for _ in range(replays):
+        g.replay()
+    e1.record(cur)
+    e1.synchronize()
+    wall = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1)
+    # the collectives alone: T all-gathers of buffer 0, back to back, in a graph
+    ga = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize(dev)
+    with torch.cuda.graph(ga, stream=s):
+        for _ in range(T):
+            gather.start(0)
+            gather.wait(0)
+    ga.replay()
+    torch.cuda.synchronize(dev)
+    a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a0.record(cur)
+    for _ in range(replays):
+        ga.replay()
+    a1.record(cur)
+    a1.synchronize()
+    alone_ms = a0.elapsed_time(a1) / (replays * T)
+    t = torch.tensor([ms, wall * 1e3, alone_ms], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms, wall_ms, alone_ms = t.tolist()
+    del g, ga
+    recv = gather.chunk * world
+    steps = replays * T
+    return {"replays": replays, "steps": steps, "ms_per_step": round(ms / steps, 6),
+            "host_wall_ms_per_step": round(wall_ms / steps, 6),
+            "collective_alone_us": round(alone_ms * 1e3, 3),
+            "collective_alone_recv_gbs": round(recv / (alone_ms * 1e-3) / 1e9, 1),
+            "note": "per replay: the reset, %d steps and %d all-gathers (max over ranks); the collective alone: "
+                    "%d all-gathers of one buffer per replay" % (T, T, T)}
 
 
 def graph_episode_run(torch, env, reset, lib, nat, a_ptr, o_ptr, r_ptr, per_t, n, T, dev, replays=10):

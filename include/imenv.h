@@ -359,6 +359,12 @@ int imenv_poisson_table(const ImEnv* env, uint32_t* out, int32_t cap, int32_t* l
  * in-transit ring (one row of n envs per node and lead-time slot: the sum of the delays). */
 int imenv_state_layout(const ImEnv* env, int32_t* elem_bytes, int32_t* row_len, int32_t* ring_depth);
 
+/* Divergent split state layout (trees, IM_div_env.py:396-502 / MAIM_div_env.py:476-579 backlog_to):
+ * the number of split children (nodes whose parent ships to more than one child; only they carry a
+ * backlog_to) and its element bytes (2 = int16 when num_periods x the children's order_max fits 32767,
+ * else 4). 0 children for serial chains. */
+int imenv_split_layout(const ImEnv* env, int32_t* num_split_children, int32_t* elem_bytes);
+
 /* Host-fed noisy-delay uniforms for ONE period (device double [N][n]) written into the table that
  * reset(delay_uniforms=...) fills, so a caller can draw them lazily, step by step, in the
  * reference's order (np.random.uniform per node, factory first, IM_env.py:384-407) and keep its

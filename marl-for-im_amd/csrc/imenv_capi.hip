@@ -485,6 +485,13 @@ int64_t state_bound(const ImEnvSpec& s) {
   return B;
 }
 
+// Largest magnitude of a split child's backlog_to (the reference's signed per-child backlog, IM_div_env.py
+// :396-502): each period adds at most the child's order (<= order_max: A adds the unshipped part of it,
+// C and D add order - ship_to with ship_to >= 0, B adds nothing), so backlog_to <= T x order_max. It goes
+// below zero only in case C, where a backlog-first shipment s <= backlog_to is subtracted twice (drained,
+// then order - ship_to with ship_to = s): the result is >= -backlog_to. Loops A and D decrement only
+// positive counts. So |backlog_to| <= T x order_max of the child. (validate_and_derive inlines this.)
+
 // Largest magnitude of the signed net-inventory row (inv - backlog): inventory up to its capacity or
 // initial level, backlog up to its cap or T periods of demand.
 int64_t net_bound(const ImEnvSpec& s) {
@@ -537,6 +544,19 @@ int validate_and_derive(const ImEnvSpec& s, SpecDev& d, int& maxc) {
       for (int k = 0; k < m; ++k) d.split_child[s.children[p][k]] = 1;
     }
   }
+  // compact backlog_to rows (imenv_device.h BtoRow): one slot per split child, in node order; int16 when
+  // bto_bound fits it (IMENV_BTO_BYTES=4 forces int32: testing)
+  d.num_bto = 0;
+  for (int i = 0; i < IMENV_MAX_NODES; ++i) d.bto_slot[i] = -1;
+  int64_t bto_om = 0;
+  for (int i = 0; i < N; ++i)
+    if (d.split_child[i]) {
+      d.bto_slot[i] = d.num_bto++;
+      bto_om = std::max<int64_t>(bto_om, s.order_max[i]);
+    }
+  d.bto_es = (int64_t)s.num_periods * bto_om <= 32767 ? 2 : 4;
+  if (const char* v = std::getenv("IMENV_BTO_BYTES"))
+    if (std::atoi(v) == 4) d.bto_es = 4;
   int nret = 0;
   for (int i = 0; i < N; ++i) {
     if (s.retailer_slot[i] >= 0) {
@@ -653,6 +673,23 @@ int alloc(T** p, size_t count) {
 // blocks (JitFlags::small_blocks, imenv_jit.hip jit_step_block_size)
 constexpr int64_t kSmallLaunchEnvs = 2 * 64 * 4 * 256;
 
+// State records (imenv_device.h: one 16- or 32-byte record per env holding the net and order_u rows and
+// every ring slot) for launches of at most this many envs: one wave generation, where the launch is a
+// latency chain and one 16-byte load and store per lane beats two row accesses plus one byte access per
+// node (tools/probe_small.py: 3.79 vs 3.97 us for C2's access shape at 131,072 envs). Larger launches
+// keep the rows: there the record's unused ring slots are extra bytes (104 vs 96 B per env-step for C2)
+// for no gain. IMENV_REC=0 / 1 turns records off / on at any size; IMENV_REC_MAX_ENVS moves the limit.
+int rec_bytes_for(const SpecDev& d, int64_t n) {
+  const int N = d.s.num_nodes;
+  const int need = 2 * d.np + d.ring_total;
+  if (d.es != 1 || N > 8 || need > 32) return 0;
+  int64_t lim = kSmallLaunchEnvs;
+  if (const char* v = std::getenv("IMENV_REC_MAX_ENVS")) lim = std::atoll(v);
+  if (const char* v = std::getenv("IMENV_REC")) lim = std::atoi(v) != 0 ? INT64_MAX : -1;
+  if (n > lim) return 0;
+  return need <= 16 ? 16 : 32;
+}
+
 int64_t wt_state_limit() {
   static const int64_t lim = [] {
     const char* v = std::getenv("IMENV_WT_STATE_MAX_BYTES");
@@ -683,7 +720,8 @@ struct ImEnv {
   int maxc = 0;
   size_t es = 4;       // state element size (1, 2 or 4)
   void *d_net = nullptr, *d_ou = nullptr, *d_ring = nullptr, *d_hist_d = nullptr, *d_hist_o = nullptr;
-  int32_t *d_carry = nullptr, *d_bto = nullptr, *d_demand = nullptr;
+  int32_t *d_carry = nullptr, *d_demand = nullptr;
+  void* d_bto = nullptr;   // compact backlog_to rows [n][row_len(num_bto)] of bto_es bytes
   double* d_delay_u = nullptr;
   float* d_lut32 = nullptr;
   double* d_lut64 = nullptr;
@@ -765,10 +803,15 @@ int imenv_create(const ImEnvSpec* spec, int64_t n_envs, int64_t env_offset, int 
   hipError_t he = hipSetDevice(device);
   if (he != hipSuccess) { delete h; return fail(IMENV_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(he)); }
   char **net = reinterpret_cast<char**>(&h->d_net), **ou = reinterpret_cast<char**>(&h->d_ou),
-       **ring = reinterpret_cast<char**>(&h->d_ring);
-  if ((rc = alloc(&h->d_spec, 1)) || (rc = alloc(net, rowb)) || (rc = alloc(ou, rowb)) ||
-      (rc = alloc(ring, n * h->es * h->host.ring_total)) || (rc = alloc(&h->d_carry, n * np)) ||
-      (rc = alloc(&h->d_bto, h->maxc > 0 ? n * np : 0)) || (rc = alloc(&h->d_err, n)) ||
+       **ring = reinterpret_cast<char**>(&h->d_ring), **bto = reinterpret_cast<char**>(&h->d_bto);
+  const int nbt = h->host.num_bto;
+  h->host.rec_bytes = rec_bytes_for(h->host, n_envs);
+  const bool rec = h->host.rec_bytes > 0;
+  const size_t bto_row = (size_t)h->host.bto_es * (h->host.bto_es == 2 ? ((nbt + 1) & ~1) : nbt);
+  if ((rc = alloc(&h->d_spec, 1)) || (rc = alloc(net, rec ? n * h->host.rec_bytes : rowb)) ||
+      (rc = alloc(ou, rec ? 0 : rowb)) || (rc = alloc(ring, rec ? 0 : n * h->es * h->host.ring_total)) ||
+      (rc = alloc(&h->d_carry, n * np)) ||
+      (rc = alloc(bto, h->maxc > 0 ? n * bto_row : 0)) || (rc = alloc(&h->d_err, n)) ||
       (rc = alloc(&h->d_err_any, 1)) || (rc = alloc(&h->d_episode, 1))) {
     imenv_destroy(h);
     return rc;
@@ -902,7 +945,9 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
   A.noisy_delay_thr = h->noisy_thr;
   A.noisy_delay_thr32 = prob_thr32(h->noisy_thr);
   A.noisy_demand_thr32 = prob_thr32(s.noisy_demand_threshold);
-  for (int i = 0; i < s.num_nodes; ++i) A.ring_at[i] = (int64_t)(h->host.ring_off[i] + h->t % s.delay[i]) * h->n;
+  for (int i = 0; i < s.num_nodes; ++i)   // rows: element offset of the slot's row; records: the slot's byte
+    A.ring_at[i] = h->host.rec_bytes ? (int64_t)(2 * h->host.np + h->host.ring_off[i] + h->t % s.delay[i])
+                                     : (int64_t)(h->host.ring_off[i] + h->t % s.delay[i]) * h->n;
   LaunchCfg c;
   c.mc = h->maxc;
   c.base = is_base_obs(s);
@@ -1260,7 +1305,11 @@ int imenv_get_state(ImEnv* h, int32_t* inv, int32_t* backlog, int32_t* order_u, 
   } else {
     const unsigned grid = (unsigned)((h->n + 255) / 256);
     // inventory and backlog are the two sides of the signed net row (imenv_device.h, NetOf)
-    if (h->host.es == 1)
+    if (h->host.rec_bytes)   // state records: net row at byte 0, order_u row at byte np, record stride
+      hipLaunchKernelGGL((imenv_state_kernel<int8_t, uint8_t>), dim3(grid), dim3(256), 0, st,
+                         static_cast<const int8_t*>(h->d_net), static_cast<const uint8_t*>(h->d_net) + h->host.np,
+                         inv, backlog, order_u, h->n, h->host.rec_bytes, s.num_nodes);
+    else if (h->host.es == 1)
       hipLaunchKernelGGL((imenv_state_kernel<int8_t, uint8_t>), dim3(grid), dim3(256), 0, st,
                          static_cast<const int8_t*>(h->d_net), static_cast<const uint8_t*>(h->d_ou), inv, backlog,
                          order_u, h->n, h->host.np, s.num_nodes);
@@ -1318,6 +1367,13 @@ int imenv_state_layout(const ImEnv* h, int32_t* elem_bytes, int32_t* row_len, in
   if (elem_bytes) *elem_bytes = (int32_t)h->es;
   if (row_len) *row_len = h->host.np;
   if (ring_depth) *ring_depth = h->host.ring_total;
+  return IMENV_OK;
+}
+
+int imenv_split_layout(const ImEnv* h, int32_t* num_split_children, int32_t* elem_bytes) {
+  if (!h) return fail(IMENV_E_INVALID, "null handle");
+  if (num_split_children) *num_split_children = h->maxc > 0 ? h->host.num_bto : 0;
+  if (elem_bytes) *elem_bytes = h->host.bto_es;
   return IMENV_OK;
 }
 
@@ -1407,6 +1463,7 @@ int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, cha
   f.wt_state = flags & 16384u;
   f.small_blocks = flags & 32768u;
   f.demand_layout = (int)((flags >> 5) & 31u);
+  d.rec_bytes = rec_bytes_for(d, f.small_blocks ? 1 : INT64_MAX);   // as a handle of that size would
   std::string msg;
   std::string src;
   if (flags & (1u << 12)) {   // the rollout kernel; bits 13..19 = RolloutFlags::key()

@@ -23,8 +23,14 @@
 //                                           arrival load and departure store hit one address and a
 //                                           wave moves whole 128-byte lines (a time-major ring
 //                                           scatters 2-byte stores that dirty partial sectors)
+//   record (small launches) [n][16|32 B]    uint8 state of up to 8 nodes as ONE record per env instead of
+//                                           the three arrays above: net row, order_u row, then every ring
+//                                           slot (node i's slot s at byte 2 NP + ring_off[i] + s), zero
+//                                           padded; one 16/32-byte load and store per lane (SpecDev::rec_bytes)
 //   hist_d / hist_o         [L][n][NP] ST   demand / order history rows (prev_* observations)
-//   backlog_to, carry       [n][NP] int32   split state (trees) / noisy-delay carry
+//   backlog_to              [n][E] int16|int32  split state of the E split children only (trees);
+//                                           int16 when T x the children's order_max fits (bto_bound)
+//   carry                   [n][NP] CarryOf<ST> noisy-delay carry
 //   actions [n][N] f32|f64, obs [n][N][F] f32|f64, reward [n] or [n][N] f64 (policy layout)
 // Build: --offload-arch=gfx950 -O3 -ffp-contract=off (no FMA contraction, IEEE division:
 // float64 rewards/obs are bit-exact with NumPy).
@@ -143,6 +149,10 @@ struct SpecDev {
   int32_t split_node[IMENV_MAX_NODES];
   int32_t split_child[IMENV_MAX_NODES];     // 1 if node's parent splits its shipment
   int32_t single_parent[IMENV_MAX_NODES];   // parent if it has exactly one child, else -1
+  int32_t num_bto;                          // split children: nodes whose parent splits its shipment
+  int32_t bto_es;                           // backlog_to element bytes: 2 (int16) or 4 (int32)
+  int32_t bto_slot[IMENV_MAX_NODES];        // node -> its slot in the compact backlog_to row, or -1
+  int32_t rec_bytes;                        // 0: state rows + ring; 16 / 32: one state record per env
   int32_t factory;
   int32_t dmax;                             // max delay
   int32_t ring_off[IMENV_MAX_NODES];        // first ring row of node i (sum of earlier delays)
@@ -171,7 +181,7 @@ struct StepArgs {
   void* ou;
   void* ring;
   void* carry;                // noisy-delay carry rows (CarryOf<ST>)
-  int32_t* bto;
+  void* bto;                  // compact backlog_to rows (BtoRow)
   void* hist_d;
   void* hist_o;
   const int32_t* demand;      // PER_ENV: [T][R][n]; BROADCAST: [T][R]
@@ -201,7 +211,8 @@ struct StepArgs {
   double noisy_delay_thr;
   uint64_t noisy_delay_thr32;
   uint64_t noisy_demand_thr32;
-  int64_t ring_at[IMENV_MAX_NODES];   // element offset of node i's ring row this step: (ring_off[i] + t mod delay[i]) * n
+  int64_t ring_at[IMENV_MAX_NODES];   // element offset of node i's ring row this step: (ring_off[i] + t mod delay[i]) * n;
+                                      // with state records: that slot's byte in the record, 2 NP + ring_off[i] + t mod delay[i]
 };
 
 // Fused base-stock rollout (imenv_base_stock_rollout): whole episodes of P policies x S demand
@@ -548,9 +559,8 @@ struct Row {
     }
   }
 
-  // write-through form for exact rows: e0 is the wave-uniform first env, lane = e - e0
-  __device__ static __forceinline__ void store_wt(ST* __restrict__ base, int64_t e0, int lane, const int (&v)[NT]) {
-    uint32_t w[WORDS];
+  // the raw words of an exact row (the inverse of unpack)
+  __device__ static __forceinline__ void pack(const int (&v)[NT], uint32_t (&w)[WORDS]) {
 #pragma unroll
     for (int q = 0; q < WORDS; ++q) w[q] = 0;
 #pragma unroll
@@ -559,6 +569,12 @@ struct Row {
       else if constexpr (ES == 2) w[i >> 1] |= ((uint32_t)(uint16_t)(int16_t)v[i]) << ((i & 1) * 16);
       else w[i] = (uint32_t)v[i];
     }
+  }
+
+  // write-through form for exact rows: e0 is the wave-uniform first env, lane = e - e0
+  __device__ static __forceinline__ void store_wt(ST* __restrict__ base, int64_t e0, int lane, const int (&v)[NT]) {
+    uint32_t w[WORDS];
+    pack(v, w);
     wt_store_words<BYTES>(wt_rsrc(base + e0 * NPT), lane * BYTES, w);
   }
 };
@@ -576,6 +592,72 @@ template <> struct NetOf<uint8_t> { using type = int8_t; };
 // when T x the state bound exceeds int16), int32 beside int16 / int32 state.
 template <typename ST> struct CarryOf { using type = int32_t; };
 template <> struct CarryOf<uint8_t> { using type = int16_t; };
+
+// The split state: backlog_to of the E = nb() split children only (a single child's and the factory's
+// are always 0), one row [n][E] of int16 (when the spec proves |backlog_to| <= T x the children's
+// order_max fits: the only decrement below zero is the reference's double subtraction of a backlog-first
+// shipment, IM_div_env.py:468-484 + 501, which is bounded by the positive part) or int32. Slot k of the
+// row belongs to the node with bto_slot(node) == k. P::NBT is the compile-time capacity: the exact E for
+// a JIT policy, NT for the ahead-of-time kernels (runtime E and element width).
+template <class P>
+struct BtoRow {
+  static constexpr int CAP = P::NBT > 0 ? P::NBT : 1;
+  using R16 = Row<int16_t, CAP, P::JIT>;
+  using R32 = Row<int32_t, CAP, P::JIT>;
+  static constexpr int WORDS = R32::WORDS;   // >= R16::WORDS
+  __device__ static __forceinline__ void load(const P& p, const void* base, int64_t e, uint32_t (&w)[WORDS]) {
+    const int nb = p.nb();
+    if (p.bto_es() == 2) {
+      uint32_t w16[R16::WORDS];
+      R16::load(static_cast<const int16_t*>(base), e, nb, nb, w16);
+#pragma unroll
+      for (int q = 0; q < WORDS; ++q) w[q] = q < R16::WORDS ? w16[q < R16::WORDS ? q : 0] : 0u;
+    } else {
+      R32::load(static_cast<const int32_t*>(base), e, nb, nb, w);
+    }
+  }
+  // node-indexed backlog_to (0 for nodes that are not split children)
+  __device__ static __forceinline__ void unpack(const P& p, const uint32_t (&w)[WORDS], int (&btoc)[P::NT]) {
+    int v[CAP];
+    if (p.bto_es() == 2) {
+      uint32_t w16[R16::WORDS];
+#pragma unroll
+      for (int q = 0; q < R16::WORDS; ++q) w16[q] = w[q];
+      R16::unpack(w16, v);
+    } else {
+      R32::unpack(w, v);
+    }
+#pragma unroll
+    for (int j = 0; j < P::NT; ++j) {
+      const int k = j < p.N() ? p.bto_slot(j) : -1;
+      btoc[j] = k >= 0 ? sel<CAP>(v, k) : 0;
+    }
+  }
+  __device__ static __forceinline__ void pack(const P& p, const int (&btoc)[P::NT], int (&v)[CAP]) {
+#pragma unroll
+    for (int k = 0; k < CAP; ++k) v[k] = 0;
+#pragma unroll
+    for (int j = 0; j < P::NT; ++j) {
+      const int k = j < p.N() ? p.bto_slot(j) : -1;
+#pragma unroll
+      for (int q = 0; q < CAP; ++q) v[q] = (k == q) ? btoc[j] : v[q];
+    }
+  }
+  __device__ static __forceinline__ void store(const P& p, void* base, int64_t e, const int (&btoc)[P::NT]) {
+    int v[CAP];
+    pack(p, btoc, v);
+    const int nb = p.nb();
+    if (p.bto_es() == 2) R16::store(static_cast<int16_t*>(base), e, nb, nb, v);
+    else R32::store(static_cast<int32_t*>(base), e, nb, nb, v);
+  }
+  // write-through form (exact rows: JIT policies)
+  __device__ static __forceinline__ void store_wt(const P& p, void* base, int64_t e0, int lane, const int (&btoc)[P::NT]) {
+    int v[CAP];
+    pack(p, btoc, v);
+    if (p.bto_es() == 2) R16::store_wt(static_cast<int16_t*>(base), e0, lane, v);
+    else R32::store_wt(static_cast<int32_t*>(base), e0, lane, v);
+  }
+};
 
 // ---------------------------------------------------------------- runtime spec policy
 // Every accessor reads the spec from device memory (scalar loads). Per-call flags come from A.
@@ -617,6 +699,13 @@ struct DynSpec {
   __device__ int single_parent(int c) const { return sp->single_parent[c]; }
   __device__ int split_child(int c) const { return sp->split_child[c]; }
   __device__ int split_node(int si) const { return sp->split_node[si]; }
+  static constexpr int NBT = NT_;                    // backlog_to row capacity (runtime count nb())
+  // state records (uint8 state, N <= 8): capacity 32 bytes, runtime size rec_words()
+  static constexpr int RECW = (sizeof(ST_) == 1 && NT_ <= 8) ? 8 : 0;
+  __device__ int rec_words() const { return RECW > 0 ? sp->rec_bytes / 4 : 0; }
+  __device__ int nb() const { return sp->num_bto; }
+  __device__ int bto_es() const { return sp->bto_es; }
+  __device__ int bto_slot(int i) const { return sp->bto_slot[i]; }
   __device__ int num_children(int p) const { return sp->s.num_children[p]; }
   __device__ int child(int p, int k) const { return sp->s.children[p][k]; }
   __device__ int split_limit(int p, int q) const { return sp->s.split_limit[p][q]; }
@@ -978,13 +1067,30 @@ __device__ __forceinline__ bool staged_obs(const P& p) {
 // block writes its contiguous obs slab with full 1 KiB-per-wave float4 stores.
 // Per-env raw words of one step, loaded before any of them is used (step_load) so that the loads
 // of all the envs a thread owns overlap; step_finish unpacks and computes.
+// State records: byte b of a record held as W raw words (b wave-uniform: a kernel argument or a
+// constant), and the same words with byte b replaced (one select per word, no branch)
+template <int W>
+__device__ __forceinline__ uint32_t rec_byte(const uint32_t (&w)[W], int b) {
+  uint32_t x = 0;
+#pragma unroll
+  for (int q = 0; q < W; ++q) x = (q == (b >> 2)) ? w[q] : x;
+  return (x >> ((b & 3) * 8)) & 0xFFu;
+}
+template <int W>
+__device__ __forceinline__ void rec_put(uint32_t (&w)[W], int b, uint32_t v) {
+  const int sh = (b & 3) * 8;
+  const uint32_t m = 0xFFu << sh;
+#pragma unroll
+  for (int q = 0; q < W; ++q) w[q] = (q == (b >> 2)) ? ((w[q] & ~m) | ((v & 0xFFu) << sh)) : w[q];
+}
+
 template <class P>
 struct StepLoad {
   using R = Row<typename P::ST, P::NT, P::EXACT>;
-  using R32 = Row<int32_t, P::NT, P::EXACT>;
   using RC = Row<typename CarryOf<typename P::ST>::type, P::NT, P::EXACT>;
   uint32_t aw[2 * P::NT];
-  uint32_t w_net[R::WORDS], w_ou[R::WORDS], w_cin[RC::WORDS], w_bto[R32::WORDS];
+  uint32_t w_net[R::WORDS], w_ou[R::WORDS], w_cin[RC::WORDS], w_bto[BtoRow<P>::WORDS];
+  uint32_t w_rec[P::RECW > 0 ? P::RECW : 1];   // the env's state record (P::RECW > 0 and rec_words() > 0)
   typename P::ST r_arr[P::NT];
   int cdem[P::NT];
   double du[P::NT];
@@ -999,7 +1105,7 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
   constexpr bool EXACT = P::EXACT;
   using ST = typename P::ST;
   using R = Row<ST, NT, EXACT>;
-  using R32 = Row<int32_t, NT, EXACT>;
+  using RB = BtoRow<P>;
   using SN = typename NetOf<ST>::type;
   using RN = Row<SN, NT, EXACT>;
   const int64_t n = A.n;
@@ -1013,13 +1119,13 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
   using CT = typename CarryOf<ST>::type;
   using RC = Row<CT, NT, EXACT>;
   const CT* __restrict__ p_carry = static_cast<const CT*>(A.carry);
-  const int32_t* __restrict__ p_bto = A.bto;
+  const void* __restrict__ p_bto = A.bto;
   // ================= (A) loads: raw words only, every independent load issued before any use
   uint32_t (&aw)[2 * NT] = L.aw;
   uint32_t (&w_net)[R::WORDS] = L.w_net;
   uint32_t (&w_ou)[R::WORDS] = L.w_ou;
   uint32_t (&w_cin)[RC::WORDS] = L.w_cin;
-  uint32_t (&w_bto)[R32::WORDS] = L.w_bto;
+  uint32_t (&w_bto)[RB::WORDS] = L.w_bto;
   ST (&r_arr)[NT] = L.r_arr;
   int (&cdem)[NT] = L.cdem;
   double (&du)[NT] = L.du;
@@ -1033,10 +1139,13 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
 #pragma unroll
   for (int q = 0; q < RC::WORDS; ++q) w_cin[q] = 0;
 #pragma unroll
-  for (int q = 0; q < R32::WORDS; ++q) w_bto[q] = 0;
+  for (int q = 0; q < RB::WORDS; ++q) w_bto[q] = 0;
 #pragma unroll
   for (int i = 0; i < NT; ++i) { cdem[i] = 0; du[i] = 1.0; r_arr[i] = 0; }
-  if constexpr (IMENV_BUF_LOAD && EXACT) {
+  const bool rec = P::RECW > 0 && p.rec_words() > 0;
+#pragma unroll
+  for (int q = 0; q < (P::RECW > 0 ? P::RECW : 1); ++q) L.w_rec[q] = 0;
+  if constexpr (IMENV_BUF_LOAD && EXACT && P::RECW == 0) {
     // buffer loads off the slab's first env: the bases are scalars, the lane's byte offset is shared by
     // every row of one element size, and lanes past n read 0 (the resource ends at the last env), so
     // no 64-bit address arithmetic and no tail clamp
@@ -1057,7 +1166,7 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
     for (int i = 0; i < NT; ++i)
       r_arr[i] = buf_load_elem<ST>(ld_rsrc(p_ring + A.ring_at[i] + e0, cnt * ES), lane * ES);
     if (p.noisy_delay()) buf_load_words<RC::BYTES>(ld_rsrc(p_carry + e0 * RC::NPT, cnt * RC::BYTES), lane * RC::BYTES, w_cin);
-    if (MC > 0) buf_load_words<R32::BYTES>(ld_rsrc(p_bto + e0 * R32::NPT, cnt * R32::BYTES), lane * R32::BYTES, w_bto);
+    if (MC > 0) RB::load(p, p_bto, valid ? e : n - 1, w_bto);
     if (p.demand_layout() == IMENV_LAYOUT_PER_ENV) {
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
@@ -1116,13 +1225,26 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
       }
     }
     // state and arrivals are loaded even at t == 0 (then ignored): unconditional, branch-free loads
-    RN::load(p_net, el, np, N, w_net);
-    R::load(p_ou, el, np, N, w_ou);
+    if constexpr (P::RECW > 0) {
+      if (rec) {   // one record: net, order_u and every ring slot (unpacked in step_finish)
+        const uint32_t* __restrict__ rb = static_cast<const uint32_t*>(A.net);
+        if (P::RECW == 4 || p.rec_words() == 4) {
+          uint32_t (&w4)[4] = *reinterpret_cast<uint32_t(*)[4]>(L.w_rec);
+          load_words<16>(rb + el * 4, w4);
+        } else if constexpr (P::RECW == 8) {
+          load_words<32>(rb + el * 8, L.w_rec);
+        }
+      }
+    }
+    if (!rec) {
+      RN::load(p_net, el, np, N, w_net);
+      R::load(p_ou, el, np, N, w_ou);
 #pragma unroll
-    for (int i = 0; i < NT; ++i)
-      if (i < N) r_arr[i] = p_ring[A.ring_at[i] + el];
+      for (int i = 0; i < NT; ++i)
+        if (i < N) r_arr[i] = p_ring[A.ring_at[i] + el];
+    }
     if (p.noisy_delay()) RC::load(p_carry, el, np, N, w_cin);
-    if (MC > 0) R32::load(p_bto, el, np, N, w_bto);
+    if (MC > 0) RB::load(p, p_bto, el, w_bto);
     if (p.demand_layout() == IMENV_LAYOUT_PER_ENV) {
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
@@ -1134,10 +1256,10 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
 #pragma unroll
       for (int i = 0; i < NT; ++i) if (i < N) du[i] = A.delay_u[((int64_t)t * N + i) * n + el];
     }
-    if constexpr (P::TD_PRE > 0) {
+    if (P::TD_PRE > 0 && !rec) {
       // time-dependent observation of period t+1: slot j < d_i - 1 of node i is ring slot
       // (t + 1 + j) mod d_i, never the slot this step overwrites (t mod d_i), so it loads here with
-      // the state instead of after the step (IM_env.py:416-432)
+      // the state instead of after the step (IM_env.py:416-432); a state record holds them already
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
 #pragma unroll
@@ -1175,7 +1297,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   constexpr int OROW = P::BASE ? 0 : P::OBS_ROW;   // general rows staged in LDS (JIT)
   using ST = typename P::ST;
   using R = Row<ST, NT, EXACT>;
-  using R32 = Row<int32_t, NT, EXACT>;
+  using RB = BtoRow<P>;
   using SN = typename NetOf<ST>::type;
   using RN = Row<SN, NT, EXACT>;
   const int tid = threadIdx.x;
@@ -1196,13 +1318,13 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   using CT = typename CarryOf<ST>::type;
   using RC = Row<CT, NT, EXACT>;
   CT* __restrict__ p_carry = static_cast<CT*>(A.carry);
-  int32_t* __restrict__ p_bto = A.bto;
+  void* __restrict__ p_bto = A.bto;
   const int64_t ring_rows = n * np;   // elements per packed-row array (history)
   const uint32_t (&aw)[2 * NT] = L.aw;
   const uint32_t (&w_net)[R::WORDS] = L.w_net;
   const uint32_t (&w_ou)[R::WORDS] = L.w_ou;
   const uint32_t (&w_cin)[RC::WORDS] = L.w_cin;
-  const uint32_t (&w_bto)[R32::WORDS] = L.w_bto;
+  const uint32_t (&w_bto)[RB::WORDS] = L.w_bto;
   const ST (&r_arr)[NT] = L.r_arr;
   const int (&cdem)[NT] = L.cdem;
   const double (&du)[NT] = L.du;
@@ -1257,17 +1379,61 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
     if (p.act_f64()) x[i] = __hiloint2double((int)aw[2 * i + 1], (int)aw[2 * i]);
     else x[i] = (double)__uint_as_float(aw[i]);
   }
-  RN::unpack(w_net, inv);
+  // a state record (small launches) holds the net and order_u rows as its first words and every ring
+  // slot after them: the arrival of node i is the byte the host names in ring_at[i]
+  constexpr int RECW = P::RECW > 0 ? P::RECW : 1;
+  const bool rec = P::RECW > 0 && p.rec_words() > 0;
+  [[maybe_unused]] const uint32_t (&w_rec)[RECW] = L.w_rec;
+  uint32_t wn[R::WORDS], wo[R::WORDS];
+  ST ra[NT];
+  [[maybe_unused]] ST rtd[NT][P::TD_PRE > 0 ? P::TD_PRE : 1];
+#pragma unroll
+  for (int q = 0; q < R::WORDS; ++q) {
+    wn[q] = w_net[q];
+    wo[q] = w_ou[q];
+  }
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    ra[i] = r_arr[i];
+#pragma unroll
+    for (int j = 0; j < (P::TD_PRE > 0 ? P::TD_PRE : 1); ++j) rtd[i][j] = r_td[i][j];
+  }
+  if constexpr (P::RECW > 0) {
+    if (rec) {
+      constexpr int RW = R::WORDS;   // = NP / 4 (uint8 rows, N == NT)
+#pragma unroll
+      for (int q = 0; q < RW; ++q) {
+        wn[q] = w_rec[q];
+        wo[q] = w_rec[RW + q];
+      }
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        ra[i] = (ST)rec_byte<RECW>(w_rec, (int)A.ring_at[i]);
+#pragma unroll
+        for (int j = 0; j < P::TD_PRE; ++j) {
+          rtd[i][j] = 0;
+          const int d = p.delay(i);
+          if (j < d - 1 && t + 1 + j - d >= 0)
+            rtd[i][j] = (ST)rec_byte<RECW>(w_rec, 8 * RW + p.ring_off(i) + (t + 1 + j) % d);
+        }
+      }
+    }
+  }
+  RN::unpack(wn, inv);
 #pragma unroll
   for (int i = 0; i < NT; ++i) {   // net -> (inv, backlog): one of them is 0
     bl[i] = max(-inv[i], 0);
     inv[i] = max(inv[i], 0);
   }
-  R::unpack(w_ou, ou);
+  R::unpack(wo, ou);
 #pragma unroll
-  for (int i = 0; i < NT; ++i) arr[i] = (int)r_arr[i];
+  for (int i = 0; i < NT; ++i) arr[i] = (int)ra[i];
   RC::unpack(w_cin, cin);
-  R32::unpack(w_bto, btoc);
+  if constexpr (MC > 0) RB::unpack(p, w_bto, btoc);
+  else {
+#pragma unroll
+    for (int i = 0; i < NT; ++i) btoc[i] = 0;
+  }
   if (t == 0) {              // period-0 state is implicit (IM_env.py:221-224); one uniform branch
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
@@ -1318,7 +1484,39 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
     int net[NT];
 #pragma unroll
     for (int i = 0; i < NT; ++i) net[i] = inv[i] - bl[i];   // inv[i] * bl[i] == 0 after step_core
-    if constexpr (IMENV_WT_STATE && EXACT) {
+    bool state_done = false;
+    if constexpr (P::RECW > 0) {
+      if (rec) {   // the whole record back: new rows, this step's departures in their ring slots
+        constexpr int RW = R::WORDS;
+        uint32_t wr[RECW], pn[RW], po[RW];
+#pragma unroll
+        for (int q = 0; q < RECW; ++q) wr[q] = w_rec[q];
+        RN::pack(net, pn);
+        R::pack(ou, po);
+#pragma unroll
+        for (int q = 0; q < RW; ++q) {
+          wr[q] = pn[q];
+          wr[RW + q] = po[q];
+        }
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+          if (i < N) rec_put<RECW>(wr, (int)A.ring_at[i], (uint32_t)push[i]);
+        uint32_t* __restrict__ rb = static_cast<uint32_t*>(A.net);
+        if (P::RECW == 4 || p.rec_words() == 4) {
+          const uint32_t (&w4)[4] = *reinterpret_cast<const uint32_t(*)[4]>(wr);
+          if constexpr (IMENV_WT_STATE) wt_store_words<16>(wt_rsrc(rb + uniform_i64(e - tid) * 4), tid * 16, w4);
+          else store_words<16>(rb + e * 4, w4);
+        } else if constexpr (P::RECW == 8) {
+          if constexpr (IMENV_WT_STATE) wt_store_words<32>(wt_rsrc(rb + uniform_i64(e - tid) * 8), tid * 32, wr);
+          else store_words<32>(rb + e * 8, wr);
+        }
+        state_done = true;
+      }
+    }
+    if (state_done) {
+      if (p.noisy_delay()) RC::store(p_carry, e, np, N, cout);
+      if constexpr (MC > 0) RB::store(p, p_bto, e, btoc);
+    } else if constexpr (IMENV_WT_STATE && EXACT) {
       const int64_t e0 = uniform_i64(e - tid);
       RN::store_wt(p_net, e0, tid, net);
       R::store_wt(p_ou, e0, tid, ou);
@@ -1330,7 +1528,10 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
         else __builtin_amdgcn_raw_buffer_store_b32((uint32_t)push[i], rr, 4 * tid, 0, CPOL_SC1);
       }
       if (p.noisy_delay()) RC::store_wt(p_carry, e0, tid, cout);
-      if (MC > 0) R32::store_wt(p_bto, e0, tid, btoc);
+      if constexpr (MC > 0) {
+        if constexpr (P::JIT) RB::store_wt(p, p_bto, e0, tid, btoc);
+        else RB::store(p, p_bto, e, btoc);
+      }
     } else {
       RN::store(p_net, e, np, N, net);
       R::store(p_ou, e, np, N, ou);
@@ -1338,7 +1539,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
       for (int i = 0; i < NT; ++i)
         if (i < N) p_ring[A.ring_at[i] + e] = (ST)push[i];
       if (p.noisy_delay()) RC::store(p_carry, e, np, N, cout);
-      if (MC > 0) R32::store(p_bto, e, np, N, btoc);
+      if constexpr (MC > 0) RB::store(p, p_bto, e, btoc);
     }
     if (!split_ok) {          // no-return atomics
       atomicOr(A.err + e, 1u);
@@ -1494,7 +1695,10 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
               v[i] = push[i];
             } else if constexpr (P::TD_PRE > 0) {
 #pragma unroll
-              for (int q = 0; q < P::TD_PRE; ++q) if (q == j) v[i] = (int)r_td[i][q];
+              for (int q = 0; q < P::TD_PRE; ++q) if (q == j) v[i] = (int)rtd[i][q];
+            } else if (rec) {
+              if constexpr (P::RECW > 0)
+                v[i] = (int)rec_byte<RECW>(w_rec, 2 * p.np() + p.ring_off(i) + (tp + j) % d);
             } else {
               v[i] = (int)p_ring[(int64_t)(p.ring_off(i) + (tp + j) % d) * n + e];
             }

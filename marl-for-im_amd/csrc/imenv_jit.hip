@@ -316,6 +316,8 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
     << "  static constexpr int RING = " << d.ring_total << ";\n"
     << "  static constexpr int OBS_ROW = " << obs_row << ";\n"
     << "  static constexpr bool OBS_STAGE64 = " << blit(f.obs_f64) << ";\n"
+    << "  static constexpr int NBT = " << d.num_bto << ";\n"
+    << "  static constexpr int RECW = " << d.rec_bytes / 4 << ";\n"
     << "  static constexpr int TD_PRE = " << (has_td && d.dmax > 1 ? d.dmax - 1 : 0) << ";\n"
     << "  static constexpr bool XCD_REMAP = " << blit(f.small_blocks) << ";\n"
     << "  using ST = " << (d.es == 1 ? "uint8_t" : d.es == 2 ? "int16_t" : "int32_t") << ";\n"
@@ -333,6 +335,9 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
   sc("int", "prev_length", ilit(s.prev_length));
   sc("int", "num_features", ilit(F));
   sc("int", "num_split", ilit(d.num_split));
+  sc("int", "nb", ilit(d.num_bto));
+  sc("int", "rec_words", ilit(d.rec_bytes / 4));
+  sc("int", "bto_es", ilit(d.bto_es));
   sc("bool", "std_actions", blit(s.standardise_actions != 0));
   sc("bool", "clip_round", blit(s.decode_mode == IMENV_DECODE_CLIP_ROUND));
   sc("double", "a", dlit(s.a));
@@ -364,6 +369,7 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
   emit1(o, "int", "demand_parent", N, I(s.demand_parent), "-1");
   emit1(o, "int", "single_parent", N, I(d.single_parent), "-1");
   emit1(o, "int", "split_child", N, I(d.split_child), "0");
+  emit1(o, "int", "bto_slot", N, I(d.bto_slot), "-1");
   emit1(o, "int", "split_node", d.num_split, I(d.split_node), "0");
   emit1(o, "int", "num_children", N, I(s.num_children), "0");
   emit1(o, "double", "sell", N, Dd(s.sell_price), "(0.0)");
@@ -470,10 +476,24 @@ std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f)
   std::ostringstream o;
   const int ept = jit_envs_per_thread(d, base, f.obs_f64);
   emit_policy(o, d, maxc, base, f, jit_step_block_size(d, base, f.obs_f64 ? 8 : 4, ept, f.small_blocks), ept);
+  // The arguments a wave needs first lead the signature as scalars, so that with kernel-argument
+  // preloading (jit_options) they arrive in SGPRs at wave launch: the loads of actions and state
+  // issue without waiting for a scalar load of the argument segment (tools/probe_launch.py: 0.30-0.37 us
+  // of a 3.5-4 us launch at 131,072 envs). StepArgs (~360 bytes, not preloadable) follows for the rest.
   o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
-    << jit_kernel_name(f) << "(const imenv::SpecDev* __restrict__ sp, const imenv::StepArgs A) {\n"
+    << jit_kernel_name(f)
+    << "(const void* __restrict__ act, void* __restrict__ state, const uint32_t* __restrict__ ep, void* __restrict__ obs,\n"
+       "    double* __restrict__ rew, int t, unsigned n32, unsigned long long ring_pack,\n"
+       "    const imenv::SpecDev* __restrict__ sp,\n"
+       "    const imenv::StepArgs A0) {\n"
        "  __shared__ uint32_t s_tab[JitSpec::TAB_LDS];\n"
        "  __shared__ __attribute__((aligned(16))) float s_obs[imenv::stage_floats<JitSpec>()];\n"
+       "  imenv::StepArgs A = A0;\n"
+       "  A.actions = act; A.net = state; A.episode = ep; A.obs = obs; A.reward = rew; A.t = t; A.n = (int64_t)n32;\n"
+       "  if constexpr (JitSpec::RECW > 0) {   // state records: byte i of ring_pack = node i's slot byte\n"
+       "#pragma unroll\n"
+       "    for (int i = 0; i < JitSpec::NT; ++i) A.ring_at[i] = (int64_t)((ring_pack >> (8 * i)) & 0xFFull);\n"
+       "  }\n"
        "  const JitSpec p(sp, A);\n"
        "  imenv::step_body(p, A, s_tab, s_obs);\n"
        "}\n";
@@ -491,8 +511,19 @@ unsigned device_src_hash() {
 }
 std::unordered_map<std::string, std::shared_ptr<const std::vector<char>>> g_code;
 
+// Kernel-argument preloading (gfx950): the leading scalar arguments of a kernel are written into SGPRs
+// when its waves launch. IMENV_JIT_PRELOAD=0 turns it off (A/B).
+bool jit_preload() {
+  const char* v = std::getenv("IMENV_JIT_PRELOAD");
+  return !(v && std::atoi(v) == 0);
+}
+
 std::vector<std::string> jit_options(const std::string& arch) {
   std::vector<std::string> v = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off"};
+  if (jit_preload()) {
+    v.push_back("-mllvm");
+    v.push_back("-amdgpu-kernarg-preload-count=16");
+  }
   if (const char* extra = std::getenv("IMENV_JIT_OPTS")) {   // tuning experiments, e.g. -DFOO=1
     std::istringstream is(extra);
     std::string w;
@@ -588,9 +619,12 @@ bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const st
   char tag[224];
   // dev=: hash of the device-code header, so a profile of an older kernel body never matches this one;
   // the kernel name carries the hash of any extra compile options
-  std::snprintf(tag, sizeof tag, "%s%s[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,ept=%d,%zuB,dev=%08x]", tag_prefix(),
-                jit_kernel_name(f).c_str(), d.s.num_nodes, maxc, base ? 1 : 0, d.es, f.key(), out.bs, out.ept,
-                src.size(), device_src_hash());
+  // rec=: state records (imenv_capi.hip rec_bytes_for), so a profile of the row layout never matches;
+  // kpre=: the hot arguments preloaded into SGPRs (a different code object, with its own profiles)
+  std::snprintf(tag, sizeof tag, "%s%s[N=%d,MC=%d,base=%d,es=%d,flags=0x%x,bs=%d,ept=%d,%s%s%zuB,dev=%08x]",
+                tag_prefix(), jit_kernel_name(f).c_str(), d.s.num_nodes, maxc, base ? 1 : 0, d.es, f.key(), out.bs,
+                out.ept, d.rec_bytes ? (d.rec_bytes == 16 ? "rec=16," : "rec=32,") : "",
+                jit_preload() ? "kpre=16," : "", src.size(), device_src_hash());
   out.tag = tag;
   return true;
 }
@@ -598,7 +632,16 @@ bool jit_load(const SpecDev& d, int maxc, bool base, const JitFlags& f, const st
 hipError_t jit_launch(const JitKernel& k, hipStream_t st, const SpecDev* sp, const StepArgs& A) {
   const SpecDev* spv = sp;
   StepArgs av = A;
-  void* args[] = {&spv, &av};
+  const void* act = A.actions;
+  void* state = A.net;
+  const uint32_t* ep = A.episode;
+  void* obs = A.obs;
+  double* rew = A.reward;
+  int t = A.t;
+  unsigned n32 = (unsigned)A.n;         // n <= 2^31 (imenv_create)
+  unsigned long long ring_pack = 0;   // state records: node i's ring byte (< 32) in byte i
+  for (int i = 0; i < 8; ++i) ring_pack |= (unsigned long long)(A.ring_at[i] & 0xFF) << (8 * i);
+  void* args[] = {&act, &state, &ep, &obs, &rew, &t, &n32, &ring_pack, &spv, &av};
   const int64_t per_block = (int64_t)k.bs * k.ept;
   const unsigned grid = (unsigned)((A.n + per_block - 1) / per_block);
   return hipModuleLaunchKernel(k.fn, grid, 1, 1, (unsigned)k.bs, 1, 1, 0, st, args, nullptr);

@@ -60,6 +60,14 @@ class PackedGather:
             off += (nbytes + _ALIGN - 1) // _ALIGN * _ALIGN
         self.chunk = off
         self.device = torch.device(device)
+        # an all-gather needs one send size on every rank: RCCL given different counts hangs or corrupts
+        # memory instead of raising, so the sizes are compared first (one collective of equal shape)
+        if self.world > 1:
+            sz = torch.tensor([off, -off], dtype=torch.int64, device=self.device)
+            dist.all_reduce(sz, op=dist.ReduceOp.MAX, group=group)
+            if int(sz[0]) != off or -int(sz[1]) != off:
+                raise ValueError("PackedGather: the ranks' send buffers differ in size (this rank %d bytes, "
+                                 "largest %d, smallest %d): shard the envs evenly" % (off, int(sz[0]), -int(sz[1])))
         self._send = [torch.empty(self.chunk, dtype=torch.uint8, device=self.device) for _ in range(buffers)]
         self._recv = [torch.empty(self.world * self.chunk, dtype=torch.uint8, device=self.device)
                       for _ in range(buffers)]

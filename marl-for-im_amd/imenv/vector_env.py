@@ -306,6 +306,12 @@ class VectorInvEnv:
         nat.check(self.lib.imenv_state_layout(self._h, byref(eb), byref(rl), byref(rd)), "imenv_state_layout")
         return eb.value, rl.value, rd.value
 
+    def split_layout(self):
+        """(split children carrying a backlog_to, its element bytes) of the HBM split state."""
+        nb, eb = c_int32(), c_int32()
+        nat.check(self.lib.imenv_split_layout(self._h, byref(nb), byref(eb)), "imenv_split_layout")
+        return nb.value, eb.value
+
     def step_traffic(self, action_bytes=4, obs_bytes=4, host_demand=False, metrics=False):
         """Algorithmic HBM bytes of one step() per env: (steady state, average over an episode)."""
         per = self.step_traffic_per_period(action_bytes, obs_bytes, host_demand, metrics)
@@ -326,17 +332,20 @@ class VectorInvEnv:
         s = self.spec
         N, T = s.num_nodes, s.num_periods
         d = [int(x) for x in s.delay]
-        split = any(len(c) > 1 for c in s.children)
+        nbto, bto_es = self.split_layout()
+        split = nbto > 0
         hist = any(g in (nat.G_DEMAND_HIST, nat.G_ORDER_HIST) and j >= 1 for g, j in s.features)
         per = []
         # noisy-delay carry rows: int16 beside uint8 state, else int32, padded to 4 bytes (CarryOf /
-        # row_len in imenv_device.h); divergent backlog_to rows: int32 [N]
+        # row_len in imenv_device.h); divergent backlog_to rows: the split children's only, int16 or int32
+        # (BtoRow), padded to 4 bytes
         cb = 2 if es == 1 else 4
         carry_row = cb * (((N + 1) & ~1) if cb == 2 else N)
+        bto_row = bto_es * (((nbto + 1) & ~1) if bto_es == 2 else nbto)
         for t in range(T):
             b = N * action_bytes + 2 * NP * es + (2 * NP * es if t > 0 else 0)
             b += es * sum(1 for i in range(N) if t >= d[i]) + N * es
-            for on, row in ((self.noisy_delay, carry_row), (split, 4 * N)):
+            for on, row in ((self.noisy_delay, carry_row), (split, bto_row)):
                 if on:
                     b += row + (row if t > 0 else 0)
             if hist:

@@ -62,8 +62,10 @@ def test_bench_json_line(steps, warmup):
     assert f64["bytes_per_env_step"] > r["bytes_per_env_step"] and f64["value"] > 0
     g = r["graph"]                   # the HIP-graph-replayed episode (informational)
     assert g["steps"] == 30 * g["replays"] and g["ms_per_step"] > 0 and g["kernel"] == r["kernel"]
-    assert d["resets_timed"] == sum(1 for s in range(warmup, warmup + steps) if s % 30 == 0)
+    ph = d["config"]["episode_phase"]
+    assert d["resets_timed"] == sum(1 for s in range(warmup, warmup + steps) if (s + ph) % 30 == 0) >= 1
     assert ("%d of them preceded by the episode's reset kernel" % d["resets_timed"]) in d["config"]["workload"]
+    assert r["reset_us"] > 0 and "resets" in d["value_basis"]
     assert d["ranks_seen"] == 1 and d["launcher"] == "none"
     assert 90 < r["bytes_per_env_step"] <= r["bytes_per_env_step_steady"]
     if steps != 20:
@@ -172,3 +174,16 @@ def test_rccl_solo_is_world_size_one_only():
     r = _run_rc(["--gpus", "2", "--rccl-solo", "--no-cpu-baseline"], timeout=60, WORLD_SIZE="2", RANK="0",
                 LOCAL_RANK="0")
     assert r.returncode == 2 and "--rccl-solo" in r.stderr
+
+
+@pytest.mark.parametrize("W,K", [(5, 20), (0, 1), (7, 29), (5, 30), (60, 300), (3, 2), (29, 10)])
+def test_timed_window_holds_a_reset(W, K):
+    """The driver's short window (--steps 20 --warmup 5) is phased so that an episode boundary, and with it
+    the reset kernel, falls inside the timed steps; windows of >= 30 steps hold one anyway."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "marl-for-im_amd"))
+    import bench
+    ph = bench.episode_phase(W, K, 30)
+    assert 0 <= ph < 30 and (ph == 0 or K < 30)
+    assert bench.resets_in_window(W, K, 30, ph) >= 1
+    assert bench.resets_in_window(W, K, 30, ph) == sum(1 for s in range(W, W + K) if (s + ph) % 30 == 0)

@@ -354,7 +354,11 @@ def test_gpu_step_traffic_matches_bench_formula():
     env.close()
     env = _env("MAIM_div", C4, 64)     # td slot of node 1 (delay 2), backlog_to rows, no history rows
     steady, _ = env.step_traffic()
-    assert steady == 16 + 16 + 4 + 1 + 4 + 32 + 96 + 8
+    # backlog_to of the two split children only (imenv_split_layout): int16 (T x order_max = 900 fits),
+    # 4 B read + 4 B written; int32 under IMENV_BTO_BYTES=4
+    nb, be = env.split_layout()
+    assert nb == 2 and be == (4 if os.environ.get("IMENV_BTO_BYTES") == "4" else 2)
+    assert steady == 16 + 16 + 4 + 1 + 4 + 2 * nb * be + 96 + 8
     env.close()
 
 

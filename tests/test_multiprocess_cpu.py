@@ -191,3 +191,28 @@ def test_metric_stats_over_ranks(tmp_path):
     # merging a single rank is the identity; empty-free uneven splits
     one = merge_column_stats(torch.tensor([[[3.0, 2.0]]]), [5])
     assert torch.allclose(one, torch.tensor([[3.0, 2.0]], dtype=torch.float64))
+
+
+def _uneven_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 5 + rank          # shard_range of an odd total: the first rank holds one env more
+        try:
+            StepGather(torch.zeros((n, 4, 3)), torch.zeros(n, dtype=torch.float64))
+            msg = None
+        except ValueError as e:
+            msg = str(e)
+        torch.save(dict(msg=msg), out_path + str(rank))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_uneven_shards_are_refused_before_any_gather(tmp_path):
+    """Ranks whose send buffers differ (uneven shards) are refused on every rank at construction, before an
+    all-gather could be handed different counts (RCCL: undefined behaviour, not an exception)."""
+    out = str(tmp_path / "uneven.pt")
+    mp.spawn(_uneven_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        msg = torch.load(out + str(r), weights_only=True)["msg"]
+        assert msg is not None and "differ in size" in msg

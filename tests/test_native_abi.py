@@ -65,6 +65,10 @@ def test_jit_specialiser_compiles_every_golden_spec():
         sets = [0, 1 | 2 | (_native.LAYOUT_PER_ENV << 5) | (16 if meta["noisy"] else 0) | 1024]
         if name in ("C2_MAIM4", "C3_IM8", "C4_MAIM_div1", "MAIM_div2_share", "IM4_td_pd_pa_L2"):
             sets += [2048, 2 | 2048]          # streaming stores (IMENV_STORE_STREAM), f32 and f64 obs
+        # small launches (64-env blocks; uint8 specs of <= 8 nodes take the 16/32-byte state records),
+        # write-through obs and state stores as the default policy picks them there, and a tree's
+        # compact backlog_to rows, with f32 and f64 observations
+        sets += [8192 | 16384 | 32768, 2 | 8192 | 16384 | 32768, 1 | 2 | (_native.LAYOUT_PER_ENV << 5) | 32768]
         for flags in sets:
             rc = lib.imenv_jit_check(ctypes.byref(spec), b"gfx950", flags, log, len(log))
             assert rc == 0, (name, flags, log.value.decode()[:2000])
