@@ -1068,20 +1068,30 @@ __device__ __forceinline__ bool staged_obs(const P& p) {
 // Per-env raw words of one step, loaded before any of them is used (step_load) so that the loads
 // of all the envs a thread owns overlap; step_finish unpacks and computes.
 // State records: byte b of a record held as W raw words (b wave-uniform: a kernel argument or a
-// constant), and the same words with byte b replaced (one select per word, no branch)
-template <int W>
+// function of the period), read or replaced through the 64-bit word pair that holds it: one 64-bit
+// shift and mask per byte, the pair chosen by a uniform compare. Ring bytes start at 2 NP, so pairs
+// below Q0 = 2 NP / 8 never hold one (a 16-byte record of 4 nodes: pair 1 only, no compare at all).
+template <int W, int Q0 = 0>
 __device__ __forceinline__ uint32_t rec_byte(const uint32_t (&w)[W], int b) {
-  uint32_t x = 0;
+  const int k = b >> 3, sh = (b & 7) * 8;
+  uint64_t c = 0;
 #pragma unroll
-  for (int q = 0; q < W; ++q) x = (q == (b >> 2)) ? w[q] : x;
-  return (x >> ((b & 3) * 8)) & 0xFFu;
+  for (int q = Q0; q < W / 2; ++q)
+    if (k == q || q == W / 2 - 1 && q == Q0) c = ((uint64_t)w[2 * q + 1] << 32) | w[2 * q];
+  return (uint32_t)(c >> sh) & 0xFFu;
 }
-template <int W>
+template <int W, int Q0 = 0>
 __device__ __forceinline__ void rec_put(uint32_t (&w)[W], int b, uint32_t v) {
-  const int sh = (b & 3) * 8;
-  const uint32_t m = 0xFFu << sh;
+  const int k = b >> 3, sh = (b & 7) * 8;
+  const uint64_t m = 0xFFull << sh, x = (uint64_t)(v & 0xFFu) << sh;
 #pragma unroll
-  for (int q = 0; q < W; ++q) w[q] = (q == (b >> 2)) ? ((w[q] & ~m) | ((v & 0xFFu) << sh)) : w[q];
+  for (int q = Q0; q < W / 2; ++q) {
+    if (k == q || q == W / 2 - 1 && q == Q0) {
+      const uint64_t c = ((((uint64_t)w[2 * q + 1] << 32) | w[2 * q]) & ~m) | x;
+      w[2 * q] = (uint32_t)c;
+      w[2 * q + 1] = (uint32_t)(c >> 32);
+    }
+  }
 }
 
 template <class P>
@@ -1408,13 +1418,13 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
       }
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
-        ra[i] = (ST)rec_byte<RECW>(w_rec, (int)A.ring_at[i]);
+        ra[i] = (ST)rec_byte<RECW, RW>(w_rec, (int)A.ring_at[i]);
 #pragma unroll
         for (int j = 0; j < P::TD_PRE; ++j) {
           rtd[i][j] = 0;
           const int d = p.delay(i);
           if (j < d - 1 && t + 1 + j - d >= 0)
-            rtd[i][j] = (ST)rec_byte<RECW>(w_rec, 8 * RW + p.ring_off(i) + (t + 1 + j) % d);
+            rtd[i][j] = (ST)rec_byte<RECW, RW>(w_rec, 8 * RW + p.ring_off(i) + (t + 1 + j) % d);
         }
       }
     }
@@ -1500,7 +1510,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
         }
 #pragma unroll
         for (int i = 0; i < NT; ++i)
-          if (i < N) rec_put<RECW>(wr, (int)A.ring_at[i], (uint32_t)push[i]);
+          if (i < N) rec_put<RECW, RW>(wr, (int)A.ring_at[i], (uint32_t)push[i]);
         uint32_t* __restrict__ rb = static_cast<uint32_t*>(A.net);
         if (P::RECW == 4 || p.rec_words() == 4) {
           const uint32_t (&w4)[4] = *reinterpret_cast<const uint32_t(*)[4]>(wr);
@@ -1698,7 +1708,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
               for (int q = 0; q < P::TD_PRE; ++q) if (q == j) v[i] = (int)rtd[i][q];
             } else if (rec) {
               if constexpr (P::RECW > 0)
-                v[i] = (int)rec_byte<RECW>(w_rec, 2 * p.np() + p.ring_off(i) + (tp + j) % d);
+                v[i] = (int)rec_byte<RECW, Row<ST, NT, EXACT>::WORDS>(w_rec, 2 * p.np() + p.ring_off(i) + (tp + j) % d);
             } else {
               v[i] = (int)p_ring[(int64_t)(p.ring_off(i) + (tp + j) % d) * n + e];
             }

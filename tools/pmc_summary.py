@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc CSVs: per-kernel mean counter values per dispatch.
 
-    python tools/pmc_summary.py OUT.json N_ENVS DIR [DIR ...] [--bench-log LOG]
+    python tools/pmc_summary.py OUT.json N_ENVS DIR [DIR ...] [--bench-log LOG] [--alt-obs-f64]
+
+--alt-obs-f64: summarise the bench line's float64-observation kernel (roofline.alt_obs_f64, the
+reference's observation dtype, timed in the same run) instead of its main kernel.
 
 Each DIR is one rocprofv3 -d output (one --pmc pass). Kernel names are shortened
 to their template head. If the calibration kernels (tools/pmc_calib.hip, 1 GiB per
@@ -54,6 +57,9 @@ def main():
         i = argv.index("--bench-log")
         bench = argv[i + 1]
         del argv[i:i + 2]
+    alt64 = "--alt-obs-f64" in argv
+    if alt64:
+        argv.remove("--alt-obs-f64")
     trace = None
     if "--trace" in argv:          # rocprofv3 --kernel-trace --stats CSV of the same bench command
         i = argv.index("--trace")
@@ -74,8 +80,13 @@ def main():
                     # a diagnostic build (IMENV_ABLATE / IMENV_STAMPS: wrong results or extra stores) must never
                     # stand in for the production kernel's traffic
                     raise SystemExit("pmc_summary: refusing a diagnostic kernel build: " + rl["kernel"])
-                res["kernel_info"] = rl["kernel"]
-                res["algorithmic_bytes_per_launch"] = rl["bytes_per_launch"]
+                if alt64:
+                    a = rl["alt_obs_f64"]
+                    res["kernel_info"] = a["kernel"]
+                    res["algorithmic_bytes_per_launch"] = a["bytes_per_env_step"] * n_envs
+                else:
+                    res["kernel_info"] = rl["kernel"]
+                    res["algorithmic_bytes_per_launch"] = rl["bytes_per_launch"]
     fac = {}
     for k, c in (("read_dword", "FETCH_SIZE"), ("read_dwordx4", "FETCH_SIZE"), ("write_dword", "WRITE_SIZE"),
                  ("write_dwordx4", "WRITE_SIZE")):
@@ -83,6 +94,8 @@ def main():
             fac[k] = CAL_BYTES / (s[k][c] * 1024.0)
     res["bytes_per_counter_kb_factor"] = fac
     step = [k for k in s if k.startswith("imenv_step_kernel") or k.startswith("imenv_step_jit")]
+    # the kernel of the summarised line: the float64-observation kernel's name ends in _o64
+    step = [k for k in step if k.endswith("_o64") == alt64] or step
     if step and "read_dword" in fac and "write_dword" in fac:
         k = step[0]
         c = s[k]
