@@ -143,39 +143,11 @@ std::string flit(float x) {
 // values outside it take the reference expression (an IEEE double division: exact for every value).
 constexpr int64_t kVerifyMax = 1 << 16;
 
-// The largest raw value an observation of group g at node i can read, restated from the state bounds
-// (imenv_capi.hip: demand_bound / state_bound): inventory and order_u are clipped to inv_max
-// (IM_env.py:328-340); backlog to its cap, else T periods of demand; demand history to the node's
-// demand bound; order history to order_max; an in-transit slot holds one shipment (backlog + demand +
-// the split's overshoot, or the factory's order); node ids to N. emit_obs_hooks emits an unguarded
-// closed form only when this bound lies inside the verified range [0, vbound] (a cross-check of
-// state_bound: a feature that read a value beyond it would keep the guarded form, exact everywhere).
-int64_t obs_source_bound(const ImEnvSpec& s, int g, int i) {
-  auto dbound = [&](int k) -> int64_t {
-    if (s.retailer_slot[k] >= 0) return s.inv_max[k];
-    int64_t b = 0;
-    for (int c = 0; c < s.num_nodes; ++c)
-      if (s.demand_parent[c] == k) b += s.order_max[c];
-    return b;
-  };
-  auto blbound = [&](int k) -> int64_t {
-    return s.backlog_cap[k] >= 0 ? (int64_t)s.backlog_cap[k] : (int64_t)s.num_periods * dbound(k);
-  };
-  switch (g) {
-    case IMENV_G_INV: return std::max<int64_t>(s.inv_max[i], s.init_inv[i]);
-    case IMENV_G_ORDER_U: return s.inv_max[i];
-    case IMENV_G_BACKLOG: return blbound(i);
-    case IMENV_G_DEMAND_HIST: return dbound(i);
-    case IMENV_G_ORDER_HIST: return s.order_max[i];
-    case IMENV_G_TRANSIT: {
-      const int par = s.parent[i];
-      if (par < 0) return s.order_max[i];
-      return blbound(par) + dbound(par) + IMENV_MAX_CHILDREN;
-    }
-    case IMENV_G_NODE_ID: return s.num_nodes;
-    default: return INT64_MAX;
-  }
-}
+// The raw values an observation can read are state values, so they lie in [0, vbound]: vbound is
+// imenv_capi.hip's state_bound, the maximum over every node of inventory / initial inventory, the capped
+// or T-period backlog, the demand bound, order_max and a shipment (backlog + demand + the split's
+// overshoot), and at least N (node ids). An unguarded closed form is emitted only when the whole of
+// [0, vbound] was verified here; otherwise the guarded form, exact for every value.
 
 void emit_obs_hooks(std::ostream& o, const SpecDev& d) {
   const ImEnvSpec& s = d.s;
@@ -194,7 +166,7 @@ void emit_obs_hooks(std::ostream& o, const SpecDev& d) {
       const bool clamp = mode == IMENV_OBS_CLAMP_SCALED;
       const bool int_clip = clamp && clip >= 0.0 && clip == std::floor(clip) && clip < (double)kVerifyMax;
       int64_t hi = d.vbound;
-      bool full = hi <= kVerifyMax && obs_source_bound(s, g, i) <= (int64_t)d.vbound;
+      bool full = hi <= kVerifyMax;
       if (clamp) {
         if (int_clip) { hi = (int64_t)clip; full = true; }   // every value is clamped to clip first
         else full = false;

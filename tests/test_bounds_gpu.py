@@ -1,5 +1,5 @@
 """State values driven to their proven bounds (the range the JIT observation closed forms are verified
-over: imenv_jit.hip emit_obs_hooks, obs_source_bound / vbound) stay bit-exact against the oracle.
+over: imenv_jit.hip emit_obs_hooks, vbound = state_bound) stay bit-exact against the oracle.
 
 Demand is set at every retailer's capacity and the actions order nothing (or everything), so
 backlogs climb to their caps (IM_div_env.py / MAIM_div_env.py: demand_max; serial: inv_max when

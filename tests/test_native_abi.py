@@ -155,9 +155,10 @@ def _dump_jit_source(cname, tmp_path, extra_env=None):
 @pytest.mark.parametrize("cname", ["C2", "C3", "C4"])
 def test_bench_kernels_use_unguarded_verified_observations(cname, tmp_path):
     """Every scaled observation value of the bench configs is emitted as a closed form verified
-    exhaustively over [0, vbound] with no per-value range guard: the values an observation reads
-    (obs_source_bound: capacities, capped backlog, demand and shipment bounds) all lie inside the
-    verified range (imenv_jit.hip emit_obs_hooks keeps the guard otherwise)."""
+    exhaustively over [0, vbound] with no per-value range guard: the values an observation reads are
+    state values, bounded by vbound (imenv_capi.hip state_bound: capacities, capped backlog, demand and
+    shipment bounds), and that whole range is verified (imenv_jit.hip emit_obs_hooks keeps the guard
+    when it cannot verify all of it)."""
     from imenv import _native
     if not os.path.exists(_native.LIB_PATH):
         pytest.skip("libimenv.so not built")
