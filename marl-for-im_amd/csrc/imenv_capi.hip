@@ -39,16 +39,30 @@ __global__ void __launch_bounds__(256) imenv_reset_kernel(const SpecDev* __restr
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (int64_t q = q0; q < n; q += stride) err[q] = 0u;
+  // the template index q mod (row words) advances by stride mod (row words) per iteration: one 64-bit
+  // division per thread instead of one per 16-byte store
   if (!obs_f64 && (row & 3) == 0) {
     const int r4 = row >> 2;
     float4* o4 = static_cast<float4*>(obs);
     const float4* tpl = reinterpret_cast<const float4*>(sp->reset_f32);
-    for (int64_t q = q0; q < total / 4; q += stride) o4[q] = tpl[q % r4];
+    int k = (int)(q0 % r4);
+    const int ks = (int)(stride % r4);
+    for (int64_t q = q0; q < total / 4; q += stride) {
+      o4[q] = tpl[k];
+      k += ks;
+      if (k >= r4) k -= r4;
+    }
   } else if (obs_f64 && (row & 1) == 0) {
     const int r2 = row >> 1;
     double2* o2 = static_cast<double2*>(obs);
     const double2* tpl = reinterpret_cast<const double2*>(sp->reset_f64);
-    for (int64_t q = q0; q < total / 2; q += stride) o2[q] = tpl[q % r2];
+    int k = (int)(q0 % r2);
+    const int ks = (int)(stride % r2);
+    for (int64_t q = q0; q < total / 2; q += stride) {
+      o2[q] = tpl[k];
+      k += ks;
+      if (k >= r2) k -= r2;
+    }
   } else {
     for (int64_t q = q0; q < total; q += stride) {
       if (obs_f64) static_cast<double*>(obs)[q] = sp->reset_f64[q % row];

@@ -6,9 +6,6 @@ Replaces, batched, the reference's policy-search loop in base_restock_policy.py:
   dfo_func(policy, env, demand=None)    :24-45  one episode -> -1/T * sum(pmf(demand) * rewards)
   optimize_inventory_policy(env, fun, init_policy=None, method='Powell', demand=None)  :48-63
 
-plus ``search_base_stock``, a population (cross-entropy) search that scores a whole generation of
-candidate policies on shared scenarios in one launch.
-
 and the base-stock evaluation loop of the experiment scripts (inv_management.py:222-232,
 inv_management_div.py). ``BaseStockRollout`` runs P policies x S demand scenarios as P*S whole
 episodes in ONE fused kernel launch (imenv_base_stock_rollout: state in registers, lead-time queue
@@ -202,48 +199,6 @@ def optimize_inventory_policy(env, fun=dfo_func, init_policy=None, method="Powel
     policy = out.x.copy()
     policy = np.round(np.maximum(policy, 0), 0).astype(int)
     return policy, out
-
-
-def search_base_stock(kind_or_spec, config=None, demand=None, n_scenarios=4096, population=64, generations=15,
-                      elite=8, init=None, init_std=None, seed=0, device=None):
-    """Population search over base-stock levels: the batched companion of optimize_inventory_policy
-    (base_restock_policy.py:48-63), which Powell-minimises dfo_func one episode per call.
-
-    Cross-entropy method: each generation draws `population` candidate level vectors from a Gaussian,
-    scores every candidate on the SAME scenarios (demand [S, T] / [S, R, T], or n_scenarios drawn
-    in-kernel with the spec's distribution) in ONE fused launch (BaseStockRollout: P x S whole
-    episodes), and refits mean and std to the `elite` best mean objectives (dfo_func's objective,
-    minimised). Candidates are clipped at 0 and rounded to integer levels before scoring (the
-    reference rounds its result the same way, base_restock_policy.py:59-61), so every score is the
-    exact mean over the scenarios of the policy that is returned. Deterministic for a given seed.
-
-    Returns (best_levels int [N], result dict: objective (mean over the scenarios), generations
-    (per-generation best mean objective), evaluations, mean, std)."""
-    ro = BaseStockRollout(kind_or_spec, config, device=device)
-    try:
-        N = ro.N
-        rs = np.random.RandomState(seed)
-        mu = np.full(N, float(ro.spec.mu if ro.spec.demand_dist == "poisson" else 5.0)) if init is None \
-            else np.asarray(init, dtype=np.float64).copy()
-        sd = np.maximum(np.asarray(ro.spec.order_max, dtype=np.float64) / 4.0, 1.0) if init_std is None \
-            else np.full(N, float(init_std)) if np.ndim(init_std) == 0 else np.asarray(init_std, dtype=np.float64)
-        kw = dict(demand=demand) if demand is not None else dict(n_scenarios=int(n_scenarios))
-        best, best_obj, hist, evals = None, np.inf, [], 0
-        for _ in range(int(generations)):
-            cand = np.rint(np.maximum(mu + sd * rs.standard_normal((int(population), N)), 0.0))
-            cand[0] = np.rint(np.maximum(mu, 0.0))          # the current mean itself is always scored
-            out = ro.run(cand, objective=True, per_episode=False, **kw)
-            score = out["stats"][:, nat.STAT_NAMES.index("objective"), 0].cpu().numpy()
-            evals += cand.shape[0]
-            order = np.argsort(score, kind="stable")
-            if score[order[0]] < best_obj:
-                best_obj, best = float(score[order[0]]), cand[order[0]].astype(int)
-            hist.append(float(score[order[0]]))
-            el = cand[order[:int(elite)]]
-            mu, sd = el.mean(axis=0), np.maximum(el.std(axis=0), 0.5)
-        return best, {"objective": best_obj, "generations": hist, "evaluations": evals, "mean": mu, "std": sd}
-    finally:
-        ro.close()
 
 
 def evaluate_base_stock(env, policy, test_demand, noisy_delay=False, noisy_delay_threshold=0.0):

@@ -203,28 +203,3 @@ def test_rollout_drawn_configs_vs_oracle(i):
     for k in STATS:
         np.testing.assert_array_equal(out[k].cpu().numpy(), ref[k], err_msg="%d %s" % (i, k))
     ro.close()
-
-
-def test_population_search_scores_exact_means():
-    """search_base_stock (a cross-entropy search scoring one generation per launch) returns a policy
-    whose reported objective is the exact mean dfo objective over the scenarios: the oracle's
-    restatement of dfo_func (oracle/base_stock.py) on the same scenarios gives the same mean
-    (within 1e-12: the kernel's block-merged mean vs NumPy's), and the search does not end worse
-    than the mean it started from (which it scores first)."""
-    from scipy.stats import poisson
-    from imenv.policy import search_base_stock
-    from oracle.base_stock import rollout
-    m = META["IM4_dfo"]
-    cfg = dict(m["config"])
-    rs = np.random.RandomState(11)
-    demand = rs.poisson(5, (96, 30))
-    best, res = search_base_stock("IM", cfg, demand=demand, population=24, generations=5, elite=6,
-                                  init=np.full(4, 12.0), seed=3, device=DEV)
-    assert best.shape == (4,) and best.dtype.kind == "i" and (best >= 0).all()
-    assert res["evaluations"] == 24 * 5 and len(res["generations"]) == 5
-    ora = rollout("IM", cfg, best[None, :].astype(np.float64), demand=demand,
-                  pmf=lambda k: poisson.pmf(k, mu=5))
-    assert abs(ora["objective"][0].mean() - res["objective"]) <= 1e-12 * max(1.0, abs(res["objective"]))
-    start = rollout("IM", cfg, np.full((1, 4), 12.0), demand=demand, pmf=lambda k: poisson.pmf(k, mu=5))
-    assert res["objective"] <= start["objective"][0].mean() + 1e-12
-    assert min(res["generations"]) == res["objective"]
