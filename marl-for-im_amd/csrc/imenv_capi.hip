@@ -704,6 +704,14 @@ int rec_bytes_for(const SpecDev& d, int64_t n) {
   return need <= 16 ? 16 : 32;
 }
 
+bool jit_slim() {
+  static const bool v = [] {
+    const char* e = std::getenv("IMENV_JIT_SLIM");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
+
 int64_t wt_state_limit() {
   static const int64_t lim = [] {
     const char* v = std::getenv("IMENV_WT_STATE_MAX_BYTES");
@@ -983,6 +991,12 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
     f.wt_state = h->store_policy == IMENV_STORE_WRITETHROUGH ||
                  (h->store_policy == IMENV_STORE_DEFAULT && wt_state_pays(s, h->n, A.obs_f64 != 0));
     f.small_blocks = h->n <= kSmallLaunchEnvs;
+    // code only for what this call uses (IMENV_JIT_SLIM=0 keeps the general kernel): a kernel without the
+    // info stores, and without tail-lane guards when every block is whole, is ~25% less code, which a
+    // launch fetches into cold instruction caches
+    const bool slim = jit_slim();
+    f.info = !slim || A.i_order != nullptr;
+    f.full = slim && h->n % 2048 == 0;
     auto it = h->jit_k.find(f.key());
     if (it == h->jit_k.end()) {
       // compiling + loading a module is not stream work: never do it while the stream is being
@@ -1476,6 +1490,8 @@ int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, cha
   f.wt_obs = flags & 8192u;
   f.wt_state = flags & 16384u;
   f.small_blocks = flags & 32768u;
+  f.info = !(flags & 65536u);
+  f.full = flags & 131072u;
   f.demand_layout = (int)((flags >> 5) & 31u);
   d.rec_bytes = rec_bytes_for(d, f.small_blocks ? 1 : INT64_MAX);   // as a handle of that size would
   std::string msg;

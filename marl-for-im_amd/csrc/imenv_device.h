@@ -675,6 +675,8 @@ struct DynSpec {
   static constexpr bool OBS_STAGE64 = false;         // float64 observations are stored directly
   static constexpr int TD_PRE = 0;                   // in-transit obs slots are loaded after the step
   static constexpr bool XCD_REMAP = false;           // (step_body)
+  static constexpr bool FULL = false;                // a tail block is possible (n not a multiple of the block)
+  static constexpr bool INFO = true;                 // info outputs are checked per call (A.i_order)
   using ST = ST_;
   const SpecDev* __restrict__ sp;
   const StepArgs& A;
@@ -1119,7 +1121,7 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
   using SN = typename NetOf<ST>::type;
   using RN = Row<SN, NT, EXACT>;
   const int64_t n = A.n;
-  const bool valid = e < n;
+  const bool valid = P::FULL || e < n;   // FULL: every block is whole (no tail lanes)
   const int N = p.N();
   const int np = p.np();
   const int t = A.t;
@@ -1312,7 +1314,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   using RN = Row<SN, NT, EXACT>;
   const int tid = threadIdx.x;
   const int64_t n = A.n;
-  const bool valid = e < n;
+  const bool valid = P::FULL || e < n;
   const int N = p.N();
   const int np = p.np();
   const int t = A.t;
@@ -1605,7 +1607,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
 #pragma unroll
       for (int i = 0; i < NT; ++i) if (i < N) row[4 + i] = macc[4 + i] + prof[i];
     }
-    if (A.i_order) {   // info (IM_env.py:345-350)
+    if (P::INFO && A.i_order) {   // info (IM_env.py:345-350); a JIT kernel without info has no such code
 #pragma unroll
       for (int i = 0; i < NT; ++i) if (i < N) {
         A.i_order[e * N + i] = order[i];
@@ -1823,8 +1825,8 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
 #pragma unroll
       for (int k = 0; k < EPT; ++k) {
         const int64_t e0 = eb + k * BS + gi * GS;
-        if (e0 < n) {
-          const int cnt = (n - e0) < GS ? (int)(n - e0) : GS;
+        if (P::FULL || e0 < n) {
+          const int cnt = (P::FULL || (n - e0) >= GS) ? GS : (int)(n - e0);
           const int total = cnt * row;
           double* gobs = static_cast<double*>(A.obs) + e0 * row;
           const double* so = reinterpret_cast<const double*>(s_obs + k * SLAB) + gi * GS * SSTR;
@@ -1861,8 +1863,8 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
 #pragma unroll
       for (int k = 0; k < EPT; ++k) {
         const int64_t e0 = eb + k * BS + gi * GS;
-        if (e0 < n) {
-          const int cnt = (n - e0) < GS ? (int)(n - e0) : GS;
+        if (P::FULL || e0 < n) {
+          const int cnt = (P::FULL || (n - e0) >= GS) ? GS : (int)(n - e0);
           const int total = cnt * row;
           float* gobs = static_cast<float*>(A.obs) + e0 * row;
           const float* so = s_obs + k * SLAB + gi * GS * SSTR;

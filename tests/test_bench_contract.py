@@ -55,8 +55,12 @@ def test_bench_json_line(steps, warmup):
     assert alt["store_policy"] == "plain" and alt["value"] > 0 and 0 < alt["frac"] < 1
     # the line names the kernel it timed: write-through obs / reward stores (0x2000), and at 2^20 envs
     # (58.7 MB of outputs per launch, more than L2) plain state rows; the informational run its own
-    assert r["kernel"].startswith("jit:imenv_step_jit_wt[") and ",flags=0x2000," in r["kernel"]
-    assert alt["kernel"].startswith("jit:imenv_step_jit[") and ",flags=0x0," in alt["kernel"]
+    import re
+    flags = lambda k: int(re.search(r",flags=(0x[0-9a-f]+),", k).group(1), 16)
+    # JitFlags bits: 0x2000 write-through obs, 0x4000 write-through state, 0x10000 no info code (none
+    # requested), 0x20000 whole blocks (2^20 is a multiple of 2048)
+    assert r["kernel"].startswith("jit:imenv_step_jit_wt[") and flags(r["kernel"]) == 0x2000 | 0x10000 | 0x20000
+    assert alt["kernel"].startswith("jit:imenv_step_jit[") and flags(alt["kernel"]) == 0x10000 | 0x20000
     f64 = r["alt_obs_f64"]           # the reference's float64 observations, same run (informational)
     assert f64["kernel"].startswith("jit:imenv_step_jit_wt_o64[") and 0 < f64["frac"] < 1
     assert f64["bytes_per_env_step"] > r["bytes_per_env_step"] and f64["value"] > 0
