@@ -765,7 +765,10 @@ struct ImEnv {
   std::string arch;
   std::unordered_map<uint32_t, imenv::JitKernel> jit_k;
   std::string jit_err;
-  std::string last_kernel;
+  std::string last_kernel;   // the last AOT kernel's tag (a JIT launch names its kernel through last_jit)
+  const imenv::JitKernel* last_jit = nullptr;   // entries of jit_k stay put (node-based map)
+  uint32_t cached_key = 0xFFFFFFFFu;            // the previous call's JitFlags key and kernel: no lookup
+  const imenv::JitKernel* cached_jit = nullptr; // when consecutive steps use the same flags
   // base-stock rollout: kernels per RolloutFlags, scratch for per-episode metrics and block sums
   std::unordered_map<uint32_t, imenv::JitKernel> roll_k;
   double* d_roll_part = nullptr;
@@ -997,7 +1000,15 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
     const bool slim = jit_slim();
     f.info = !slim || A.i_order != nullptr;
     f.full = slim && h->n % 2048 == 0;
-    auto it = h->jit_k.find(f.key());
+    const uint32_t key = f.key();
+    if (key == h->cached_key && h->cached_jit && h->cached_jit->fn) {   // the per-step fast path
+      HIPCHK(imenv::jit_launch(*h->cached_jit, st, h->d_spec, A));
+      h->last_jit = h->cached_jit;
+      h->t += 1;
+      if (done_out) *done_out = h->t >= s.num_periods ? 1 : 0;
+      return IMENV_OK;
+    }
+    auto it = h->jit_k.find(key);
     if (it == h->jit_k.end()) {
       // compiling + loading a module is not stream work: never do it while the stream is being
       // captured into a graph (that launch takes the ahead-of-time kernel instead)
@@ -1019,7 +1030,9 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
     }
     if (it != h->jit_k.end() && it->second.fn) {
       HIPCHK(imenv::jit_launch(it->second, st, h->d_spec, A));
-      h->last_kernel = it->second.tag;
+      h->last_jit = &it->second;
+      h->cached_key = key;
+      h->cached_jit = &it->second;
       h->t += 1;
       if (done_out) *done_out = h->t >= s.num_periods ? 1 : 0;
       return IMENV_OK;
@@ -1030,6 +1043,7 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
     std::snprintf(tag, sizeof tag, "aot:imenv_step_kernel[NT=%d,MC=%d,base=%d,es=%d]", N <= 8 ? N : 16, c.mc,
                   c.base ? 1 : 0, c.es);
     h->last_kernel = tag;
+    h->last_jit = nullptr;
   }
   switch (N) {   // exact kernels for N <= 8, padded NT = 16 above
     case 1: imenv::launch_step_nt<1>(c, h->d_spec, A); break;
@@ -1451,8 +1465,9 @@ int imenv_set_jit(ImEnv* h, int mode) {
 
 int imenv_kernel_info(const ImEnv* h, char* buf, int64_t len) {
   if (!h || !buf || len < 1) return fail(IMENV_E_INVALID, "null argument");
-  std::string s = h->last_kernel.empty() ? std::string(h->jit ? "jit (no step yet)" : "aot (no step yet)")
-                                         : h->last_kernel;
+  std::string s = h->last_jit ? h->last_jit->tag
+                 : h->last_kernel.empty() ? std::string(h->jit ? "jit (no step yet)" : "aot (no step yet)")
+                                          : h->last_kernel;
   if (!h->jit_err.empty()) s += " | jit failed: " + h->jit_err;
   if (!h->last_rollout.empty()) s += " | rollout " + h->last_rollout;
   std::snprintf(buf, (size_t)len, "%s", s.c_str());
