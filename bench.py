@@ -26,6 +26,11 @@ reported under "gather".
 The reference's own parallelism is one env per RLlib worker process (hyperparams.py:14,
 MA_inv_management.py:172); the rank processes replace those workers.
 
+Launch-bound batches (C5's 131,072-env shard, C3, C4: the host's per-step enqueue is a large part of the
+kernel's time) run the timed K steps as one HIP graph captured before the timed region and replayed once
+inside it (`--launch auto`, the default; `eager` / `graph` force one form); the metric's 2^20-env line is
+launched eagerly, one host launch per step. roofline.launch_pacing says which form ran.
+
 Prints ONE JSON line on rank 0 (keys per the driver contract), with "roofline" (step
 kernel: algorithmic bytes / HIP-event-timed kernel duration vs 8 TB/s; plus an
 informational HIP-graph-replayed episode) and "cpu_baseline" (the oracle port, one env
@@ -176,6 +181,54 @@ def pmc_traffic(n_envs, kernel):
     """HBM bytes per step-kernel launch from the committed PMC summary of this kernel variant, else None."""
     d = pmc_record(n_envs, kernel)
     return float(d["hbm_bytes_per_launch"]) if d and "hbm_bytes_per_launch" in d else None
+
+
+# ----------------------------------------------------------------- HIP events
+class HipEvent:
+    """A timing event of the HIP runtime torch itself loaded (libamdhip64.so.7, one copy per process),
+    recorded through ctypes: ~1 us of host time per record against ~10-20 us for torch.cuda.Event.record,
+    which the timed region of a small launch (3.6 us per step at 131,072 envs) cannot afford."""
+    _lib = None
+
+    @classmethod
+    def lib(cls):
+        if cls._lib is None:
+            import ctypes
+            lib = ctypes.CDLL("libamdhip64.so.7")
+            lib.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+            lib.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            lib.hipEventSynchronize.argtypes = [ctypes.c_void_p]
+            lib.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+            lib.hipEventDestroy.argtypes = [ctypes.c_void_p]
+            cls._lib = lib
+        return cls._lib
+
+    def __init__(self):
+        import ctypes
+        self.h = ctypes.c_void_p()
+        if self.lib().hipEventCreate(ctypes.byref(self.h)) != 0:
+            raise RuntimeError("hipEventCreate failed")
+        self._rec = self._lib.hipEventRecord
+        self.hv = self.h.value
+
+    def record(self, stream_ptr):
+        if self._rec(self.hv, stream_ptr) != 0:
+            raise RuntimeError("hipEventRecord failed")
+
+    def elapsed_time(self, end):
+        """ms from this event to `end` (both completed)."""
+        import ctypes
+        self._lib.hipEventSynchronize(end.hv)
+        ms = ctypes.c_float()
+        if self._lib.hipEventElapsedTime(ctypes.byref(ms), self.hv, end.hv) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return ms.value
+
+    def __del__(self):
+        try:
+            self._lib.hipEventDestroy(self.hv)
+        except Exception:
+            pass
 
 
 # ----------------------------------------------------------------- launcher
@@ -355,6 +408,10 @@ def main():
                     help="store policy of the step kernel (imenv_set_store_policy)")
     ap.add_argument("--no-alt-store", action="store_true", help="skip the informational run of the other policy")
     ap.add_argument("--no-graph", action="store_true", help="skip the informational HIP-graph episode replay")
+    ap.add_argument("--launch", default="auto", choices=["auto", "eager", "graph"],
+                    help="how the timed K steps reach the GPU: one host launch per step (eager), or the K steps "
+                         "captured beforehand into one HIP graph and replayed once (graph); auto: graph where the "
+                         "host's per-step enqueue is at least 30%% of the kernel (launch-bound small batches)")
     ap.add_argument("--no-alt-obs", action="store_true", help="skip the informational float64-observation run")
     ap.add_argument("--cpu-only", action="store_true", help=argparse.SUPPRESS)
     # rehearsal of the multi-rank path on a one-GPU box: every rank on device 0, gloo for the
@@ -457,7 +514,7 @@ def main():
     # pass, so no collective wait lies between them.
     obs64 = {}     # float64 observation buffers of the informational alt_obs_f64 leg (made on demand)
 
-    def run(first, steps, events=None, gather=None, f64=False):
+    def run(first, steps, events=None, gather=None, f64=False, sp=None, resets_here=True):
         """Steps first .. first+steps-1 of the bench's step sequence (period t = (step + phase) mod T). With a
         StepGather the env writes into its send buffers and step s's all-gather runs under step s+1;
         with f64 the observations are float64 (the reference's dtype). Returns the number of resets it
@@ -465,27 +522,29 @@ def main():
         pair = None
         resets = 0
         op, od = (obs64["ptr"], nat.F64) if f64 else (o_ptr, nat.F32)
+        step, F32 = lib.imenv_step, nat.F32      # (locals: the loop is host-paced at small launches)
+        sptr_ = sptr if sp is None else sp       # the stream the steps go to (a capture stream for graphs)
         for s in range(first, first + steps):
             t = (s + phase) % T
-            if t == 0:
-                reset(sptr)
+            if t == 0 and resets_here:
+                reset(sptr_)
                 resets += 1
             if events is not None and pair is None:
                 pair = [pool.pop(), pool.pop(), []]     # pre-created in timed()
-                pair[0].record(stream)
+                pair[0].record(sptr_)
             if pair is not None:
                 pair[2].append(t)
             if gather is None:
-                rc = lib.imenv_step(h, a_ptr[t], nat.F32, op[t], od, r_ptr[t], None, None, sptr)
+                rc = step(h, a_ptr[t], F32, op[t], od, r_ptr[t], None, None, sptr_)
             else:
                 # the env writes straight into the packed send buffer of step s (double-buffered); the
                 # all-gather of step s runs on the collective's stream under step s+1
                 rc = lib.imenv_step(h, a_ptr[t], nat.F32, gather.obs_out(s).data_ptr(), nat.F32,
-                                    gather.reward_out(s).data_ptr(), None, None, sptr)
+                                    gather.reward_out(s).data_ptr(), None, None, sptr_)
             if rc:
                 nat.check(rc, "imenv_step")
             if pair is not None and (t == T - 1 or s == first + steps - 1):
-                pair[1].record(stream)
+                pair[1].record(sptr_)
                 events.append(pair)
                 pair = None
             if gather is not None:
@@ -520,6 +579,7 @@ def main():
         e1.record(stream)
         e1.synchronize()
         us_per_cycle = e0.elapsed_time(e1) * 1e3 / 200000
+        us_per_cycle_cal[:] = [us_per_cycle]
         n_cal = 2 * T
         torch.cuda._sleep(int(3000 / us_per_cycle))       # 3 ms: longer than enqueueing n_cal steps
         e0.record(stream)
@@ -544,6 +604,24 @@ def main():
         return 0, h, g
 
     spin_info = {}
+    window_info = {}
+    graph_span = []            # launch=graph: [span ms, resets, periods of the timed steps]
+    reset_cache = []
+
+    def reset_alone_us():
+        """The reset kernel alone (us per launch): 20 back-to-back resets queued behind a busy-wait, HIP events
+        on the kernel's stream. Leaves the handle at period 0 (every timed() pass re-positions it)."""
+        if not reset_cache:
+            torch.cuda.synchronize(dev)
+            r0, r1 = HipEvent(), HipEvent()
+            torch.cuda._sleep(2000000)
+            r0.record(sptr)
+            for _ in range(20):
+                reset(sptr)
+            r1.record(sptr)
+            reset_cache.append(r0.elapsed_time(r1) * 1e3 / 20)
+        return reset_cache[0]
+    us_per_cycle_cal = []      # GPU busy-wait cycles -> us (lead_spin's calibration)
 
     def bracket(body):
         """The driver's timed region: barrier + synchronise, then body(), then synchronise; the wall time
@@ -554,10 +632,14 @@ def main():
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         out = body()
+        t1 = time.perf_counter()
         torch.cuda.synchronize(dev)
-        el = time.perf_counter() - t0
+        t2 = time.perf_counter()
+        el = t2 - t0
         if dist_on:
             dist.barrier()
+        # where the window's wall time went (host side): enqueueing the K steps, then waiting for the GPU
+        window_info.update(host_enqueue_us=round((t1 - t0) * 1e6, 1), sync_wait_us=round((t2 - t1) * 1e6, 1))
         return el, out
 
     def max_over_ranks(*xs):
@@ -581,29 +663,84 @@ def main():
         timed), max over ranks."""
         warm(W, f64=f64)
         spin, h_us, g_us = lead_spin(W, K, f64)
+        # auto: a graph where the host's per-step enqueue (measured with the GPU idle) is at least 30% of the
+        # GPU's per-step time; with the GPU running, the host's enqueue takes up to twice as long (kernel
+        # arguments written over PCIe into device memory), so an eager window of such launches is host-paced
+        # (C4 at 131,072 envs: 3.3 vs 5.8 us per step, eager kernel_us 9.0 in the driver's window)
+        graph = args.launch == "graph" or (args.launch == "auto" and h_us == h_us and h_us > 0.3 * g_us)
         if not spin_info:      # the line's own timed region (not the informational alt-store run)
             spin_info.update(host_us_per_step=None if h_us != h_us else round(h_us, 3),
                              gpu_us_per_step_queued=None if g_us != g_us else round(g_us, 3),
-                             lead_spin_cycles=spin)
-        # the timed region's event pairs, created (and their HIP events allocated by one record
-        # each) before it starts: one pair per run of steps between resets
-        pool[:] = [torch.cuda.Event(enable_timing=True) for _ in range(2 * (K // T + 2))]
+                             lead_spin_cycles=0 if graph else spin, launch="graph" if graph else "eager")
+        # the timed region's event pairs (raw HIP events: HipEvent), created and recorded once before it
+        # starts: one pair per run of steps between resets
+        pool[:] = [HipEvent() for _ in range(2 * (K // T + 2))]
         for e in pool:
-            e.record(stream)
+            e.record(sptr)
         torch.cuda.synchronize(dev)
         events = []
+        span_ms = None
+        if graph:
+            # launch-bound small batches (C5's 131,072-env shard: 3.3-9 us of host work per launch against
+            # 3.6-3.8 us of kernel, so an eager window is paced by the host): the same K steps and resets,
+            # captured into ONE HIP graph before the timed region (the handle's host period advances at
+            # capture, its device state at replay) and replayed once inside it. Same kernels, same arguments,
+            # same order; the host submits them in one call. HIP events recorded inside a captured graph do
+            # not time reliably here, and one graph per run of steps between resets costs ~10 us of GPU-side
+            # gap per replay (both measured: profiles/r05/launch_modes/), so the kernel time is the span of
+            # events around the replay minus the window's resets (reset_us, timed alone in this run), over K.
+            # A 20 us busy-wait lead lets the host submit the graph before the GPU reaches the first event.
+            cur = torch.cuda.current_stream(dev).cuda_stream
+            cs = torch.cuda.Stream(dev)
+            gph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gph, stream=cs):
+                resets = run(W, K, f64=f64, sp=torch.cuda.current_stream(dev).cuda_stream)
+            torch.cuda.synchronize(dev)
+            ga, gb = HipEvent(), HipEvent()
+            lead = int(20.0 / us_per_cycle_cal[0]) if us_per_cycle_cal else 0
 
-        def body():
-            if spin:
-                torch.cuda._sleep(spin)
-            return run(W, K, events, f64=f64)
-        el, resets = bracket(body)
+            def replay():
+                if lead:
+                    torch.cuda._sleep(lead)
+                ga.record(cur)
+                gph.replay()
+                gb.record(cur)
+            el, _ = bracket(replay)
+            span_ms = ga.elapsed_time(gb)
+            del gph
+            ts = [(W + k + phase) % T for k in range(K)]
+            graph_span[:] = [span_ms, resets, ts]
+        else:
+            def body():
+                if spin:
+                    torch.cuda._sleep(spin)
+                return run(W, K, events, f64=f64)
+            el, resets = bracket(body)
+        if graph:
+            launches = K
+            kern_ms = None            # (span - resets x reset_us) / K once the reset is timed (below)
+            first_last = span_ms
+            ksrc = ("HIP events around the one graph replay of the window, minus resets_timed x reset_us, over K "
+                    "(launch=graph)")
+            bpl = sum((per_t64 if f64 else per_t)[t] for t in graph_span[2]) * n / K
+        else:
+            launches = sum(len(ts) for _, _, ts in events)
+            kern_ms = sum(a.elapsed_time(b) for a, b, _ in events) / launches
+            first_last = events[0][0].elapsed_time(events[-1][1])
+            ksrc = "HIP event pairs around each run of step launches between resets"
+        if not spin_info.get("window"):      # the line's own timed region
+            spin_info["window"] = dict(window_info, gpu_span_us=round(first_last * 1e3, 1), wall_us=round(el * 1e6, 1),
+                                       kernel_us_source=ksrc)
         # per-launch kernel time and the algorithmic bytes of exactly the launches that were timed
         pt = per_t64 if f64 else per_t
-        kern_ms = sum(a.elapsed_time(b) for a, b, _ in events) / sum(len(ts) for _, _, ts in events)
-        bpl = sum(pt[t] for _, _, ts in events for t in ts) * n / sum(len(ts) for _, _, ts in events)
+        if not graph:
+            bpl = sum(pt[t] for _, _, ts in events for t in ts) * n / launches
+        if kern_ms is None:
+            rus = reset_alone_us()
+            kern_ms = (span_ms - resets * rus * 1e-3) / K
+            spin_info["window"]["reset_us_subtracted"] = round(resets * rus, 3)
         el, kern_ms = max_over_ranks(el, kern_ms)
-        return el, kern_ms, bpl, sum(len(ts) for _, _, ts in events), resets
+        return el, kern_ms, bpl, launches, resets
 
     def timed_gather(W, K, gather):
         """The same W + K step sequence with C5's per-step all-gather pipelined under the next step (a
@@ -621,19 +758,9 @@ def main():
     el, kern_ms, bytes_per_launch, launches, resets_timed = timed(W, K)
     kinfo = env.kernel_info()          # the timed kernel (before the informational runs below)
 
-    # the reset kernel alone (informational; the line's value already holds resets_timed of them): R
-    # back-to-back resets queued behind a busy-wait, HIP events on the kernel's stream
-    reset_us = None
-    if hasattr(torch.cuda, "_sleep"):
-        torch.cuda.synchronize(dev)
-        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda._sleep(2000000)
-        r0.record(stream)
-        for _ in range(20):
-            reset(sptr)
-        r1.record(stream)
-        r1.synchronize()
-        reset_us = r0.elapsed_time(r1) * 1e3 / 20
+    # the reset kernel alone (the line's value already holds resets_timed of them): 20 back-to-back
+    # resets queued behind a busy-wait, HIP events on the kernel's stream
+    reset_us = reset_alone_us() if hasattr(torch.cuda, "_sleep") else None
 
     gather_info = None
     if gather_on and args.scaling == "strong" and global_envs % world:

@@ -78,6 +78,23 @@ def test_bench_json_line(steps, warmup):
     assert c["value"] > 0 and c["kind"] == "port" and c["cores"] >= 1
 
 
+@pytest.mark.gpu
+def test_small_launch_window_runs_as_one_graph():
+    """C5's per-GPU shard (131,072 envs) at the driver's settings: the host's per-step enqueue is close to the
+    kernel's time, so the timed K steps (and their reset) replay as one HIP graph captured before the timed
+    region; the kernel time is the replay's event span minus the timed resets, over K."""
+    d = _run(["--n-envs", "131072", "--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--no-alt-store",
+              "--no-alt-obs", "--no-graph"], timeout=300)
+    r = d["roofline"]
+    p = r["launch_pacing"]
+    assert p["launch"] == "graph" and d["resets_timed"] == 1 and r["kernel_samples"] == 20
+    assert "graph replay" in p["window"]["kernel_us_source"] and p["window"]["reset_us_subtracted"] > 0
+    assert 0 < r["frac"] < 1 and r["kernel_us"] > 0 and d["value"] > 0
+    d = _run(["--n-envs", "131072", "--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--no-alt-store",
+              "--no-alt-obs", "--no-graph", "--launch", "eager"], timeout=300)
+    assert d["roofline"]["launch_pacing"]["launch"] == "eager" and d["roofline"]["kernel_samples"] == 20
+
+
 def _run_rc(args, timeout, **extra_env):
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1", **extra_env)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
