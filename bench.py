@@ -781,9 +781,12 @@ def main():
                                pipelined_ms_per_step=round(g_el / K * 1e3, 6),
                                pipelined_over_gather_free=round(el / g_el, 4),
                                pipelined_form="eager: one host launch per step and per collective")
-            if backend == "nccl":
+            if backend == "nccl" and world == 1:
                 # the same pipeline with the host out of the loop: one episode's reset, T steps and T
-                # all-gathers captured into one HIP graph and replayed
+                # all-gathers captured into one HIP graph and replayed. One rank only (--rccl-solo): with
+                # more ranks the per-step collective is bound by the xGMI links (58.7 MB received per rank
+                # per step at N = 8), not by the host, and a capture that failed on one rank while the
+                # others replayed would leave their collectives waiting for it
                 try:
                     gg = graph_gather_run(torch, dist, dev, gth, reset, lib, nat, a_ptr, T, h)
                     gather_info["graph"] = gg
