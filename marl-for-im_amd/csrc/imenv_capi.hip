@@ -1000,6 +1000,9 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
     const bool slim = jit_slim();
     f.info = !slim || A.i_order != nullptr;
     f.full = slim && h->n % 2048 == 0;
+    // a 16-byte aligned observation buffer and whole blocks: every group's contiguous run (64 or BS envs
+    // x the row) then starts on a 16-byte boundary and is a whole number of 16-byte words
+    f.aligned = f.full && (reinterpret_cast<uintptr_t>(obs) & 15) == 0;
     const uint32_t key = f.key();
     if (key == h->cached_key && h->cached_jit && h->cached_jit->fn) {   // the per-step fast path
       HIPCHK(imenv::jit_launch(*h->cached_jit, st, h->d_spec, A));
@@ -1507,6 +1510,7 @@ int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, cha
   f.small_blocks = flags & 32768u;
   f.info = !(flags & 65536u);
   f.full = flags & 131072u;
+  f.aligned = flags & 262144u;
   f.demand_layout = (int)((flags >> 5) & 31u);
   d.rec_bytes = rec_bytes_for(d, f.small_blocks ? 1 : INT64_MAX);   // as a handle of that size would
   std::string msg;

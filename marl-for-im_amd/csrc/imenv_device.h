@@ -677,6 +677,7 @@ struct DynSpec {
   static constexpr bool XCD_REMAP = false;           // (step_body)
   static constexpr bool FULL = false;                // a tail block is possible (n not a multiple of the block)
   static constexpr bool INFO = true;                 // info outputs are checked per call (A.i_order)
+  static constexpr bool ALIGNED = false;             // observation alignment is checked per group
   using ST = ST_;
   const SpecDev* __restrict__ sp;
   const StepArgs& A;
@@ -1831,7 +1832,9 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           double* gobs = static_cast<double*>(A.obs) + e0 * row;
           const double* so = reinterpret_cast<const double*>(s_obs + k * SLAB) + gi * GS * SSTR;
           // 16-byte stores need a 16-byte aligned destination (a caller's obs_out view may be offset)
-          if ((total & 1) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0) {
+          // (ALIGNED: the host checked the observation buffer's 16-byte alignment for this kernel; every
+          // group's run then starts on a 16-byte boundary, so the value-by-value fallback is not compiled)
+          if (P::ALIGNED || ((total & 1) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0)) {
             double2* g2 = reinterpret_cast<double2*>(gobs);
             if (IMENV_SLAB_BATCH && cnt == GS) {   // a whole group (as the float32 write-out below)
               constexpr int QT = row * GS / 2;
@@ -1868,7 +1871,7 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
           const int total = cnt * row;
           float* gobs = static_cast<float*>(A.obs) + e0 * row;
           const float* so = s_obs + k * SLAB + gi * GS * SSTR;
-          if ((total & 3) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0) {
+          if (P::ALIGNED || ((total & 3) == 0 && (reinterpret_cast<unsigned long long>(gobs) & 15) == 0)) {
             float4* g4 = reinterpret_cast<float4*>(gobs);
             // 16-byte word q of the group's contiguous output, read from the slab
             auto rq = [&](int q) -> float4 {

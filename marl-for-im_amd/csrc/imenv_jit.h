@@ -35,11 +35,13 @@ struct JitFlags {
   bool small_blocks = false;  // a launch of at most two waves per SIMD: 64-env blocks (imenv_jit.hip)
   bool info = true;           // info outputs requested (else the kernel carries no info-store code)
   bool full = false;          // n is a multiple of 2048 (so of every block size): no tail lanes
+  bool aligned = false;       // 16-byte aligned observation buffer with whole-word rows per group
   uint32_t key() const {
     return (act_f64 ? 1u : 0u) | (obs_f64 ? 2u : 0u) | (noisy_delay ? 4u : 0u) | (noisy_demand ? 8u : 0u) |
            (has_delay_u ? 16u : 0u) | ((uint32_t)demand_layout << 5) | (metrics ? 1024u : 0u) |
            (stream_store ? 2048u : 0u) | (wt_obs ? 8192u : 0u) | (wt_state ? 16384u : 0u) |
-           (small_blocks ? 32768u : 0u) | (info ? 0u : 65536u) | (full ? 131072u : 0u);
+           (small_blocks ? 32768u : 0u) | (info ? 0u : 65536u) | (full ? 131072u : 0u) |
+           (aligned ? 262144u : 0u);
   }
 };
 

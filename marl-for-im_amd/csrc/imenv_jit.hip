@@ -294,6 +294,7 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
     << "  static constexpr bool XCD_REMAP = " << blit(f.small_blocks) << ";\n"
     << "  static constexpr bool FULL = " << blit(f.full) << ";\n"
     << "  static constexpr bool INFO = " << blit(f.info) << ";\n"
+    << "  static constexpr bool ALIGNED = " << blit(f.aligned) << ";\n"
     << "  using ST = " << (d.es == 1 ? "uint8_t" : d.es == 2 ? "int16_t" : "int32_t") << ";\n"
     << "  const imenv::SpecDev* __restrict__ sp;\n"
     << "  template <class X> __device__ JitSpec(const imenv::SpecDev* __restrict__ s, const X&) : sp(s) {}\n";

@@ -58,9 +58,9 @@ def test_bench_json_line(steps, warmup):
     import re
     flags = lambda k: int(re.search(r",flags=(0x[0-9a-f]+),", k).group(1), 16)
     # JitFlags bits: 0x2000 write-through obs, 0x4000 write-through state, 0x10000 no info code (none
-    # requested), 0x20000 whole blocks (2^20 is a multiple of 2048)
-    assert r["kernel"].startswith("jit:imenv_step_jit_wt[") and flags(r["kernel"]) == 0x2000 | 0x10000 | 0x20000
-    assert alt["kernel"].startswith("jit:imenv_step_jit[") and flags(alt["kernel"]) == 0x10000 | 0x20000
+    # requested), 0x20000 whole blocks (2^20 is a multiple of 2048), 0x40000 16-byte aligned obs buffer
+    assert r["kernel"].startswith("jit:imenv_step_jit_wt[") and flags(r["kernel"]) == 0x2000 | 0x70000
+    assert alt["kernel"].startswith("jit:imenv_step_jit[") and flags(alt["kernel"]) == 0x70000
     f64 = r["alt_obs_f64"]           # the reference's float64 observations, same run (informational)
     assert f64["kernel"].startswith("jit:imenv_step_jit_wt_o64[") and 0 < f64["frac"] < 1
     assert f64["bytes_per_env_step"] > r["bytes_per_env_step"] and f64["value"] > 0

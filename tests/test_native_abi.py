@@ -69,7 +69,8 @@ def test_jit_specialiser_compiles_every_golden_spec():
         # write-through obs and state stores as the default policy picks them there, and a tree's
         # compact backlog_to rows, with f32 and f64 observations
         sets += [8192 | 16384 | 32768, 2 | 8192 | 16384 | 32768, 1 | 2 | (_native.LAYOUT_PER_ENV << 5) | 32768,
-                 8192 | 16384 | 32768 | 65536 | 131072, 2 | 8192 | 65536 | 131072]   # slim: no info, whole blocks
+                 8192 | 16384 | 32768 | 65536 | 131072, 2 | 8192 | 65536 | 131072,   # slim: no info, whole blocks
+                 8192 | 16384 | 32768 | 65536 | 131072 | 262144, 2 | 8192 | 65536 | 131072 | 262144]   # + aligned
         for flags in sets:
             rc = lib.imenv_jit_check(ctypes.byref(spec), b"gfx950", flags, log, len(log))
             assert rc == 0, (name, flags, log.value.decode()[:2000])
