@@ -365,6 +365,13 @@ int imenv_state_layout(const ImEnv* env, int32_t* elem_bytes, int32_t* row_len, 
  * else 4). 0 children for serial chains. */
 int imenv_split_layout(const ImEnv* env, int32_t* num_split_children, int32_t* elem_bytes);
 
+/* Drawn-demand layout (IMENV_LAYOUT_DRAW, IM_env.py:194-200 / IM_div_env.py:235-255 demand draws): 0 when
+ * every step draws its own period's demand, else the element bytes (1 = uint8, 2 = int16, 4 = int32) of a
+ * [num_periods][num_retailers][n] table through which the step at t % 4 == 0 hands the demand of periods
+ * t+1..t+3 (the rest of its Philox block; same values) to the next three steps. Chosen at imenv_create for
+ * small single-retailer handles (<= 131,072 envs; IMENV_DTAB / IMENV_DTAB_MAX_ENVS override). */
+int imenv_draw_layout(const ImEnv* env, int32_t* elem_bytes);
+
 /* Host-fed noisy-delay uniforms for ONE period (device double [N][n]) written into the table that
  * reset(delay_uniforms=...) fills, so a caller can draw them lazily, step by step, in the
  * reference's order (np.random.uniform per node, factory first, IM_env.py:384-407) and keep its

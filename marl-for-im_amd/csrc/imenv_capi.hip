@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstddef>
 #include <cstdint>
 #include <cstdlib>
 #include <cstdio>
@@ -704,6 +705,32 @@ int rec_bytes_for(const SpecDev& d, int64_t n) {
   return need <= 16 ? 16 : 32;
 }
 
+// Drawn-demand table for launches of at most this many envs, where the step kernel is a latency chain
+// and its demand draw (a Philox block on the episode word, then the inversion) sits on it: C2 at
+// 131,072 envs 3.91 -> 3.40 us per launch without the draw (profiles/r05/ablate). A Philox block gives
+// four periods, so the step at t % 4 == 0 draws all four and parks the next three in the table
+// (imenv_device.h step_finish); the other three steps read one element per retailer. (Drawing the whole
+// episode in the reset instead costs a VALU-bound kernel of 11-17 us per episode, more than the steps
+// save; profiles/r05/dtab.) Measured in the graph-replayed window: C2 at 131,072 envs 3.97 -> 3.87 us
+// per launch on average; C4 (two retailers: eight inversions at t % 4 == 0) 5.49 -> 5.99, so by default
+// the table is for a single retailer only. The element is the narrowest integer holding every value a
+// draw makes: [0, table_len] for Poisson, [low, high) for uniform, doubled when demand is noisy.
+// IMENV_DTAB=0 / 1 turns it off / on at any size and retailer count; IMENV_DTAB_MAX_ENVS moves the limit.
+int dtab_es_for(const SpecDev& d, int64_t n) {
+  const ImEnvSpec& s = d.s;
+  if (s.demand_dist != IMENV_DEMAND_POISSON && s.demand_dist != IMENV_DEMAND_UNIFORM) return 0;
+  int64_t lim = s.num_retailers == 1 ? kSmallLaunchEnvs : -1;
+  if (const char* v = std::getenv("IMENV_DTAB_MAX_ENVS")) lim = std::atoll(v);
+  if (const char* v = std::getenv("IMENV_DTAB")) lim = std::atoi(v) != 0 ? INT64_MAX : -1;
+  if (n > lim) return 0;
+  int64_t lo = 0, hi = d.table_len;
+  if (s.demand_dist == IMENV_DEMAND_UNIFORM) { lo = s.uniform_low; hi = s.uniform_high; }
+  if (s.noisy_demand) { lo = std::min<int64_t>(std::min<int64_t>(lo, 2 * lo), 0); hi = std::max<int64_t>(hi, 2 * hi); }
+  if (lo >= 0 && hi <= 255) return 1;
+  if (lo >= -32768 && hi <= 32767) return 2;
+  return 4;
+}
+
 bool jit_slim() {
   static const bool v = [] {
     const char* e = std::getenv("IMENV_JIT_SLIM");
@@ -744,6 +771,7 @@ struct ImEnv {
   void *d_net = nullptr, *d_ou = nullptr, *d_ring = nullptr, *d_hist_d = nullptr, *d_hist_o = nullptr;
   int32_t *d_carry = nullptr, *d_demand = nullptr;
   void* d_bto = nullptr;   // compact backlog_to rows [n][row_len(num_bto)] of bto_es bytes
+  void* d_dtab = nullptr;  // the episode's drawn demand [T][R][n] of dtab_es bytes (dtab_es_for)
   double* d_delay_u = nullptr;
   float* d_lut32 = nullptr;
   double* d_lut64 = nullptr;
@@ -794,7 +822,7 @@ void imenv_destroy(ImEnv* h) {
   (void)hipSetDevice(h->device);
   void* ptrs[] = {h->d_spec, h->d_net, h->d_ou, h->d_ring, h->d_carry, h->d_bto, h->d_hist_d,
                   h->d_hist_o, h->d_demand, h->d_delay_u, h->d_err, h->d_err_any, h->d_lut32, h->d_lut64,
-                  h->d_episode, h->d_roll_part, h->d_roll_terms, h->d_stamps};
+                  h->d_episode, h->d_roll_part, h->d_roll_terms, h->d_stamps, h->d_dtab};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& kv : h->jit_k)
@@ -831,13 +859,15 @@ int imenv_create(const ImEnvSpec* spec, int64_t n_envs, int64_t env_offset, int 
        **ring = reinterpret_cast<char**>(&h->d_ring), **bto = reinterpret_cast<char**>(&h->d_bto);
   const int nbt = h->host.num_bto;
   h->host.rec_bytes = rec_bytes_for(h->host, n_envs);
+  h->host.dtab_es = dtab_es_for(h->host, n_envs);
   const bool rec = h->host.rec_bytes > 0;
   const size_t bto_row = (size_t)h->host.bto_es * (h->host.bto_es == 2 ? ((nbt + 1) & ~1) : nbt);
   if ((rc = alloc(&h->d_spec, 1)) || (rc = alloc(net, rec ? n * h->host.rec_bytes : rowb)) ||
       (rc = alloc(ou, rec ? 0 : rowb)) || (rc = alloc(ring, rec ? 0 : n * h->es * h->host.ring_total)) ||
       (rc = alloc(&h->d_carry, n * np)) ||
       (rc = alloc(bto, h->maxc > 0 ? n * bto_row : 0)) || (rc = alloc(&h->d_err, n)) ||
-      (rc = alloc(&h->d_err_any, 1)) || (rc = alloc(&h->d_episode, 1))) {
+      (rc = alloc(&h->d_err_any, 1)) || (rc = alloc(&h->d_episode, 1)) ||
+      (rc = alloc(reinterpret_cast<char**>(&h->d_dtab), n * s.num_periods * s.num_retailers * (size_t)h->host.dtab_es))) {
     imenv_destroy(h);
     return rc;
   }
@@ -957,6 +987,7 @@ int imenv_step(ImEnv* h, const void* actions, int action_dtype, void* obs, int o
   A.lut32 = h->d_lut32;
   A.lut64 = h->d_lut64;
   A.episode = h->d_episode;
+  A.dtab = (h->demand_layout == IMENV_LAYOUT_DRAW && h->host.dtab_es > 0) ? h->d_dtab : nullptr;
   A.metrics = h->d_metrics;
   A.stamps = h->d_stamps;
   A.n = h->n;
@@ -1415,6 +1446,12 @@ int imenv_state_layout(const ImEnv* h, int32_t* elem_bytes, int32_t* row_len, in
   return IMENV_OK;
 }
 
+int imenv_draw_layout(const ImEnv* h, int32_t* elem_bytes) {
+  if (!h) return fail(IMENV_E_INVALID, "null handle");
+  if (elem_bytes) *elem_bytes = h->host.dtab_es;
+  return IMENV_OK;
+}
+
 int imenv_split_layout(const ImEnv* h, int32_t* num_split_children, int32_t* elem_bytes) {
   if (!h) return fail(IMENV_E_INVALID, "null handle");
   if (num_split_children) *num_split_children = h->maxc > 0 ? h->host.num_bto : 0;
@@ -1513,6 +1550,7 @@ int imenv_jit_check(const ImEnvSpec* spec, const char* arch, uint32_t flags, cha
   f.aligned = flags & 262144u;
   f.demand_layout = (int)((flags >> 5) & 31u);
   d.rec_bytes = rec_bytes_for(d, f.small_blocks ? 1 : INT64_MAX);   // as a handle of that size would
+  d.dtab_es = dtab_es_for(d, f.small_blocks ? 1 : INT64_MAX);
   std::string msg;
   std::string src;
   if (flags & (1u << 12)) {   // the rollout kernel; bits 13..19 = RolloutFlags::key()

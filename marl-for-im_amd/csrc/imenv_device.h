@@ -153,6 +153,8 @@ struct SpecDev {
   int32_t bto_es;                           // backlog_to element bytes: 2 (int16) or 4 (int32)
   int32_t bto_slot[IMENV_MAX_NODES];        // node -> its slot in the compact backlog_to row, or -1
   int32_t rec_bytes;                        // 0: state rows + ring; 16 / 32: one state record per env
+  int32_t dtab_es;                          // 0: every step draws its period's demand; 1 (uint8) / 2 / 4: the
+                                            // step at t % 4 == 0 parks periods t+1..t+3 in a [T][R][n] table
   int32_t factory;
   int32_t dmax;                             // max delay
   int32_t ring_off[IMENV_MAX_NODES];        // first ring row of node i (sum of earlier delays)
@@ -185,6 +187,8 @@ struct StepArgs {
   void* hist_d;
   void* hist_o;
   const int32_t* demand;      // PER_ENV: [T][R][n]; BROADCAST: [T][R]
+  void* dtab;                 // drawn demand, [T][R][n] of SpecDev::dtab_es bytes (LAYOUT_DRAW), or null: read at
+                              // t % 4 != 0, written (periods t+1..t+3) at t % 4 == 0
   const double* delay_u;      // [T][N][n] or null
   uint32_t* err;              // [n]
   uint32_t* err_any;          // [1]
@@ -706,6 +710,7 @@ struct DynSpec {
   // state records (uint8 state, N <= 8): capacity 32 bytes, runtime size rec_words()
   static constexpr int RECW = (sizeof(ST_) == 1 && NT_ <= 8) ? 8 : 0;
   __device__ int rec_words() const { return RECW > 0 ? sp->rec_bytes / 4 : 0; }
+  __device__ int dtab_es() const { return sp->dtab_es; }
   __device__ int nb() const { return sp->num_bto; }
   __device__ int bto_es() const { return sp->bto_es; }
   __device__ int bto_slot(int i) const { return sp->bto_slot[i]; }
@@ -1264,6 +1269,19 @@ __device__ __forceinline__ void step_load(const P& p, const StepArgs& A, const i
         const int r = (i < N) ? p.retailer_slot(i) : -1;
         if (r >= 0) cdem[i] = A.demand[((int64_t)t * p.num_retailers() + r) * n + el];
       }
+    } else if (p.demand_layout() == IMENV_LAYOUT_DRAW && p.dtab_es() > 0 && (t & 3) != 0) {
+      // this period's drawn demand, drawn three periods ago or less by the step at the Philox block's
+      // first period (step_finish): one byte / short / word per retailer instead of a block and an inversion
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const int r = (i < N) ? p.retailer_slot(i) : -1;
+        if (r >= 0) {
+          const int64_t q = ((int64_t)t * p.num_retailers() + r) * n + el;
+          if (p.dtab_es() == 1) cdem[i] = static_cast<const uint8_t*>(A.dtab)[q];
+          else if (p.dtab_es() == 2) cdem[i] = static_cast<const int16_t*>(A.dtab)[q];
+          else cdem[i] = static_cast<const int32_t*>(A.dtab)[q];
+        }
+      }
     }
     if (p.has_delay_u()) {
 #pragma unroll
@@ -1319,8 +1337,17 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   const int N = p.N();
   const int np = p.np();
   const int t = A.t;
-  const bool poisson = p.demand_layout() == IMENV_LAYOUT_DRAW && p.demand_dist() == IMENV_DEMAND_POISSON;
-  const uint32_t ep = (IMENV_ABLATE & 32) ? 0u : *A.episode;   // (diagnostic: no scalar load of the episode word)
+  // drawn demand: one Philox block gives four periods (word t & 3). With a demand table (dtab, small
+  // launches) the step at a block's first period draws all four and parks the next three periods' demand
+  // in the table, which the next three steps read (`cached`): three of four steps have no draw on their
+  // latency chain. Without it every step draws its own word.
+  const bool pre = p.demand_layout() == IMENV_LAYOUT_DRAW && p.dtab_es() > 0;
+  const bool cached = pre && (t & 3) != 0;
+  const bool draw_here = p.demand_layout() == IMENV_LAYOUT_DRAW && !cached;
+  const bool poisson = draw_here && p.demand_dist() == IMENV_DEMAND_POISSON;
+  const bool need_ep = draw_here || (p.noisy_demand() && !cached) || (p.noisy_delay() && !p.has_delay_u());
+  // (diagnostic IMENV_ABLATE & 32: no scalar load of the episode word)
+  const uint32_t ep = ((IMENV_ABLATE & 32) || !need_ep) ? 0u : *A.episode;
   const uint32_t gid = A.env_offset + (uint32_t)e;
   const uint64_t seed = p.seed();
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
@@ -1363,7 +1390,41 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
     if (i < N) {
       const int r = p.retailer_slot(i);
       if (r >= 0) {
-        if (p.demand_layout() == IMENV_LAYOUT_DRAW) {
+        if (draw_here && pre) {   // t % 4 == 0: this period's demand, the next three periods' into the table
+          const uint4 b = rng_block(gid, ep, t, STREAM_DEMAND, r, k0, k1);
+          uint4 b2 = make_uint4(0u, 0u, 0u, 0u), bz = b2;
+          if (p.noisy_demand()) {
+            b2 = rng_block(gid, ep, t, STREAM_ND_DOUBLE, r, k0, k1);
+            bz = rng_block(gid, ep, t, STREAM_ND_ZERO, r, k0, k1);
+          }
+          int c4[4];
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const uint32_t x = word_of(b, w);
+            if (poisson) {
+              c4[w] = (IMENV_ABLATE & 2) ? 5 : p.poisson_draw(x, s_tab);
+            } else {
+              const uint64_t rng = (uint64_t)(p.uniform_high() - p.uniform_low());
+              c4[w] = p.uniform_low() + (int)(((uint64_t)x * rng) >> 32);
+            }
+            if (p.noisy_demand()) {   // IM_div_env.py:246-255: double, then zero
+              if ((uint64_t)word_of(b2, w) < A.noisy_demand_thr32) c4[w] = 2 * c4[w];
+              if ((uint64_t)word_of(bz, w) < A.noisy_demand_thr32) c4[w] = 0;
+            }
+          }
+          cdraw[i] = c4[0];
+          if (P::FULL || e < n) {
+#pragma unroll
+            for (int w = 1; w < 4; ++w) {
+              if (t + w < p.T()) {
+                const int64_t q = ((int64_t)(t + w) * p.num_retailers() + r) * n + e;
+                if (p.dtab_es() == 1) static_cast<uint8_t*>(A.dtab)[q] = (uint8_t)c4[w];
+                else if (p.dtab_es() == 2) static_cast<int16_t*>(A.dtab)[q] = (int16_t)c4[w];
+                else static_cast<int32_t*>(A.dtab)[q] = c4[w];
+              }
+            }
+          }
+        } else if (draw_here) {
           const uint32_t w = rng_word(gid, ep, t, STREAM_DEMAND, r, k0, k1);
           if (poisson) {
             cdraw[i] = (IMENV_ABLATE & 2) ? 5 : p.poisson_draw(w, s_tab);
@@ -1372,7 +1433,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
             cdraw[i] = p.uniform_low() + (int)(((uint64_t)w * rng) >> 32);
           }
         }
-        if (p.noisy_demand()) {
+        if (p.noisy_demand() && !pre) {   // (with a table, the draw above applied it, or the table holds it)
           const uint32_t wd = rng_word(gid, ep, t, STREAM_ND_DOUBLE, r, k0, k1);
           const uint32_t wz = rng_word(gid, ep, t, STREAM_ND_ZERO, r, k0, k1);
           nd_double[i] = (uint64_t)wd < A.noisy_demand_thr32;
@@ -1470,10 +1531,10 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
       const int r = p.retailer_slot(i);
       if (r >= 0) {
         int cd;
-        if (p.demand_layout() == IMENV_LAYOUT_PER_ENV) cd = cdem[i];
+        if (p.demand_layout() == IMENV_LAYOUT_PER_ENV || cached) cd = cdem[i];
         else if (p.demand_layout() == IMENV_LAYOUT_BROADCAST) cd = A.demand[t * p.num_retailers() + r];
         else cd = cdraw[i];
-        if (p.noisy_demand()) {   // IM_div_env.py:246-255: double, then zero
+        if (p.noisy_demand() && !pre) {   // IM_div_env.py:246-255: double, then zero
           if (nd_double[i]) cd = 2 * cd;
           if (nd_zero[i]) cd = 0;
         }

@@ -290,6 +290,7 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
     << "  static constexpr bool OBS_STAGE64 = " << blit(f.obs_f64) << ";\n"
     << "  static constexpr int NBT = " << d.num_bto << ";\n"
     << "  static constexpr int RECW = " << d.rec_bytes / 4 << ";\n"
+    << "  static constexpr bool DTAB = " << blit(d.dtab_es > 0 && f.demand_layout == IMENV_LAYOUT_DRAW) << ";\n"
     << "  static constexpr int TD_PRE = " << (has_td && d.dmax > 1 ? d.dmax - 1 : 0) << ";\n"
     << "  static constexpr bool XCD_REMAP = " << blit(f.small_blocks) << ";\n"
     << "  static constexpr bool FULL = " << blit(f.full) << ";\n"
@@ -313,6 +314,7 @@ void emit_policy(std::ostream& o, const SpecDev& d, int maxc, bool base, const J
   sc("int", "nb", ilit(d.num_bto));
   sc("int", "rec_words", ilit(d.rec_bytes / 4));
   sc("int", "bto_es", ilit(d.bto_es));
+  sc("int", "dtab_es", ilit(d.dtab_es));
   sc("bool", "std_actions", blit(s.standardise_actions != 0));
   sc("bool", "clip_round", blit(s.decode_mode == IMENV_DECODE_CLIP_ROUND));
   sc("double", "a", dlit(s.a));
@@ -457,14 +459,17 @@ std::string jit_source(const SpecDev& d, int maxc, bool base, const JitFlags& f)
   // of a 3.5-4 us launch at 131,072 envs). StepArgs (~360 bytes, not preloadable) follows for the rest.
   o << "extern \"C\" __global__ void __launch_bounds__(JitSpec::BS)\n"
     << jit_kernel_name(f)
-    << "(const void* __restrict__ act, void* __restrict__ state, const uint32_t* __restrict__ ep, void* __restrict__ obs,\n"
+    << "(const void* __restrict__ act, void* __restrict__ state, void* __restrict__ aux, void* __restrict__ obs,\n"
        "    double* __restrict__ rew, int t, unsigned n32, unsigned long long ring_pack,\n"
        "    const imenv::SpecDev* __restrict__ sp,\n"
        "    const imenv::StepArgs A0) {\n"
        "  __shared__ uint32_t s_tab[JitSpec::TAB_LDS];\n"
        "  __shared__ __attribute__((aligned(16))) float s_obs[imenv::stage_floats<JitSpec>()];\n"
        "  imenv::StepArgs A = A0;\n"
-       "  A.actions = act; A.net = state; A.episode = ep; A.obs = obs; A.reward = rew; A.t = t; A.n = (int64_t)n32;\n"
+       "  A.actions = act; A.net = state; A.obs = obs; A.reward = rew; A.t = t; A.n = (int64_t)n32;\n"
+       "  // the third hot argument: the drawn-demand table when the handle has one (the episode word then comes\n"
+       "  // with the struct), else the episode word\n"
+       "  if constexpr (JitSpec::DTAB) A.dtab = aux; else A.episode = static_cast<const uint32_t*>(aux);\n"
        "  if constexpr (JitSpec::RECW > 0) {   // state records: byte i of ring_pack = node i's slot byte\n"
        "#pragma unroll\n"
        "    for (int i = 0; i < JitSpec::NT; ++i) A.ring_at[i] = (int64_t)((ring_pack >> (8 * i)) & 0xFFull);\n"
@@ -609,14 +614,14 @@ hipError_t jit_launch(const JitKernel& k, hipStream_t st, const SpecDev* sp, con
   StepArgs av = A;
   const void* act = A.actions;
   void* state = A.net;
-  const uint32_t* ep = A.episode;
+  void* aux = A.dtab ? A.dtab : const_cast<uint32_t*>(A.episode);   // (see jit_source: JitSpec::DTAB)
   void* obs = A.obs;
   double* rew = A.reward;
   int t = A.t;
   unsigned n32 = (unsigned)A.n;         // n <= 2^31 (imenv_create)
   unsigned long long ring_pack = 0;   // state records: node i's ring byte (< 32) in byte i
   for (int i = 0; i < 8; ++i) ring_pack |= (unsigned long long)(A.ring_at[i] & 0xFF) << (8 * i);
-  void* args[] = {&act, &state, &ep, &obs, &rew, &t, &n32, &ring_pack, &spv, &av};
+  void* args[] = {&act, &state, &aux, &obs, &rew, &t, &n32, &ring_pack, &spv, &av};
   const int64_t per_block = (int64_t)k.bs * k.ept;
   const unsigned grid = (unsigned)((A.n + per_block - 1) / per_block);
   return hipModuleLaunchKernel(k.fn, grid, 1, 1, (unsigned)k.bs, 1, 1, 0, st, args, nullptr);

@@ -102,6 +102,7 @@ SYMBOLS = [
     ("imenv_poisson_table", c_int, [c_void_p, POINTER(c_uint32), c_int32, POINTER(c_int32)]),
     ("imenv_state_layout", c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     ("imenv_split_layout", c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32)]),
+    ("imenv_draw_layout", c_int, [c_void_p, POINTER(c_int32)]),
     ("imenv_set_delay_uniforms", c_int, [c_void_p, c_int32, c_void_p, c_void_p]),
     ("imenv_set_jit", c_int, [c_void_p, c_int]),
     ("imenv_set_store_policy", c_int, [c_void_p, c_int]),

@@ -312,6 +312,14 @@ class VectorInvEnv:
         nat.check(self.lib.imenv_split_layout(self._h, byref(nb), byref(eb)), "imenv_split_layout")
         return nb.value, eb.value
 
+    def draw_layout(self):
+        """Element bytes of the drawn-demand table (IMENV_LAYOUT_DRAW) through which the step at t % 4 == 0
+        hands periods t+1..t+3 to the next three steps, or 0 when every step draws its own period's demand
+        (imenv_draw_layout)."""
+        eb = c_int32()
+        nat.check(self.lib.imenv_draw_layout(self._h, byref(eb)), "imenv_draw_layout")
+        return eb.value
+
     def step_traffic(self, action_bytes=4, obs_bytes=4, host_demand=False, metrics=False):
         """Algorithmic HBM bytes of one step() per env: (steady state, average over an episode)."""
         per = self.step_traffic_per_period(action_bytes, obs_bytes, host_demand, metrics)
@@ -326,13 +334,15 @@ class VectorInvEnv:
         (only once t >= d_i) and departure written; the time-dependent observation's other in-transit
         slots; int32 noisy-delay carry and divergent backlog_to rows; the demand / order history rows
         (written every step, read for the features j >= 1); the observation; the reward; optional
-        host-fed demand and harness-metric rows.
+        host-fed demand and harness-metric rows; with a drawn-demand table (draw_layout), periods
+        t+1..t+3 written at t % 4 == 0 and read at the other periods.
         """
         es, NP, _ = self.state_layout()
         s = self.spec
         N, T = s.num_nodes, s.num_periods
         d = [int(x) for x in s.delay]
         nbto, bto_es = self.split_layout()
+        dtab_es = 0 if host_demand else self.draw_layout()
         split = nbto > 0
         hist = any(g in (nat.G_DEMAND_HIST, nat.G_ORDER_HIST) and j >= 1 for g, j in s.features)
         per = []
@@ -359,6 +369,8 @@ class VectorInvEnv:
             b += 8 * N if s.reward_mode == nat.REWARD_INDEPENDENT else 8
             if host_demand:
                 b += 4 * s.num_retailers
+            if dtab_es:
+                b += dtab_es * s.num_retailers * (sum(1 for w in (1, 2, 3) if t + w < T) if t % 4 == 0 else 1)
             if metrics:
                 b += 16 * (4 + N) - (8 * (4 + N) if t == 0 else 0)
             per.append(b)

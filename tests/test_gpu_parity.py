@@ -116,10 +116,26 @@ C4 = dict(num_nodes=4, connections={0: [1], 1: [2, 3], 2: [], 3: []}, num_period
                                                            demand_dist="uniform", lower_upper=(1, 9)), 4096),
                                          ("IM", dict(C3, demand_dist="uniform", lower_upper=(2, 13)), 4096),
                                          ("MAIM", dict(C2, mu=12.5, independent=True), 4096),
-                                         ("IM_div", dict(C4, mu=37.0, time_dependency=False), 4096)])
-def test_gpu_philox_rollout_matches_oracle(kind, cfg, n):
-    """In-kernel Philox demand + f32 actions over two episodes == oracle with the same counters."""
+                                         ("IM_div", dict(C4, mu=37.0, time_dependency=False), 4096),
+                                         # wider drawn-demand tables: int16 (noisy uniform up to 2 x 399),
+                                         # int32 (noisy uniform up to 2 x 19999)
+                                         ("MAIM_div", dict(C4, noisy_demand=True, noisy_demand_threshold=0.3,
+                                                           demand_dist="uniform", lower_upper=(100, 400)), 2048),
+                                         ("IM_div", dict(C4, noisy_demand=True, noisy_demand_threshold=0.2,
+                                                         demand_dist="uniform", lower_upper=(1, 20000),
+                                                         time_dependency=False), 2048)])
+@pytest.mark.parametrize("dtab", ["1", "0"])
+def test_gpu_philox_rollout_matches_oracle(kind, cfg, n, dtab, monkeypatch):
+    """Philox demand + f32 actions over two episodes == oracle with the same counters: drawn by the reset
+    into the episode's table (dtab "1", imenv_draw_layout > 0) and drawn in the step kernel (dtab "0")."""
+    monkeypatch.setenv("IMENV_DTAB", dtab)
     env = _env(kind, cfg, n, env_offset=1000)
+    es = env.draw_layout()
+    if dtab == "0":
+        assert es == 0
+    else:
+        hi = cfg.get("lower_upper", (0, 0))[1] * (2 if cfg.get("noisy_demand") else 1)
+        assert es == (4 if hi > 32767 else 2 if hi > 255 else 1)
     ora = OracleEnv(kind, cfg, n_envs=n)
     if cfg["demand_dist"] == "poisson":
         np.testing.assert_array_equal(env.poisson_table(), philox.poisson_thresholds(cfg.get("mu", 5)))
@@ -346,11 +362,15 @@ def test_gpu_jit_and_aot_continue_each_others_episode(state_bytes, monkeypatch):
 def test_gpu_step_traffic_matches_bench_formula():
     """Algorithmic bytes per env-step for the bench layouts: C2 96 B steady,
     95.5 B averaged over the 30-period episode (t = 0 reads no state rows, node i no arrival
-    before t = d_i)."""
+    before t = d_i); with a drawn-demand table (imenv_draw_layout: small handles) + one byte per
+    retailer read at t % 4 != 0 and three written at t % 4 == 0 (periods t+1..t+3: 22 + 22 bytes over
+    the episode)."""
     env = _env("MAIM", C2, 64)
     assert env.state_layout()[0] == 1
+    dt = env.draw_layout()
+    assert dt == (0 if os.environ.get("IMENV_DTAB") == "0" else 1)
     steady, avg = env.step_traffic()
-    assert steady == 96 and abs(avg - (96 - 15 / 30)) < 1e-9
+    assert steady == 96 + dt and abs(avg - (96 + dt * 44 / 30 - 15 / 30)) < 1e-9
     env.close()
     env = _env("MAIM_div", C4, 64)     # td slot of node 1 (delay 2), backlog_to rows, no history rows
     steady, _ = env.step_traffic()
@@ -358,7 +378,9 @@ def test_gpu_step_traffic_matches_bench_formula():
     # 4 B read + 4 B written; int32 under IMENV_BTO_BYTES=4
     nb, be = env.split_layout()
     assert nb == 2 and be == (4 if os.environ.get("IMENV_BTO_BYTES") == "4" else 2)
-    assert steady == 16 + 16 + 4 + 1 + 4 + 2 * nb * be + 96 + 8
+    # two retailers: no drawn-demand table by default (imenv_draw_layout; capi dtab_es_for)
+    assert env.draw_layout() == (1 if os.environ.get("IMENV_DTAB") == "1" else 0)
+    assert steady == 16 + 16 + 4 + 1 + 4 + 2 * nb * be + 96 + 8 + env.draw_layout() * env.spec.num_retailers
     env.close()
 
 
