@@ -839,6 +839,7 @@ def main():
     # measured stream-copy ceiling at the step's byte count: a device copy of half the
     # bytes moves them once in and once out; outside the timed region
     b_steady, b_avg = env.step_traffic()
+    b_handover = env.step_traffic(handover=True)[1] - b_avg
     half = max(1 << 20, int(b_avg * n) // 2 // 16 * 16)
     csrc = torch.empty(half // 4, dtype=torch.float32, device=dev)
     cdst = torch.empty_like(csrc)
@@ -924,6 +925,9 @@ def main():
             "bytes_per_env_step": round(bytes_per_launch / n, 3),
             "bytes_per_env_step_steady": b_steady,
             "bytes_per_env_step_episode_avg": round(b_avg, 3),
+            # drawn-demand hand-over (imenv_draw_layout): HBM bytes of that implementation choice, not
+            # algorithmic (PMC traffic includes them)
+            "handover_bytes_per_env_step_episode_avg": round(b_handover, 3),
             "bytes_per_launch": round(bytes_per_launch),
             "store_policy": args.store,
             "alt_store_policy": alt,

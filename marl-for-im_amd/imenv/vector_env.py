@@ -320,12 +320,12 @@ class VectorInvEnv:
         nat.check(self.lib.imenv_draw_layout(self._h, byref(eb)), "imenv_draw_layout")
         return eb.value
 
-    def step_traffic(self, action_bytes=4, obs_bytes=4, host_demand=False, metrics=False):
+    def step_traffic(self, action_bytes=4, obs_bytes=4, host_demand=False, metrics=False, handover=False):
         """Algorithmic HBM bytes of one step() per env: (steady state, average over an episode)."""
-        per = self.step_traffic_per_period(action_bytes, obs_bytes, host_demand, metrics)
+        per = self.step_traffic_per_period(action_bytes, obs_bytes, host_demand, metrics, handover)
         return per[-1], float(np.mean(per))
 
-    def step_traffic_per_period(self, action_bytes=4, obs_bytes=4, host_demand=False, metrics=False):
+    def step_traffic_per_period(self, action_bytes=4, obs_bytes=4, host_demand=False, metrics=False, handover=False):
         """Algorithmic HBM bytes of the step() at period t per env, for t = 0 .. T-1.
 
         The minimal traffic of this handle's layout: actions; the net-inventory
@@ -334,15 +334,17 @@ class VectorInvEnv:
         (only once t >= d_i) and departure written; the time-dependent observation's other in-transit
         slots; int32 noisy-delay carry and divergent backlog_to rows; the demand / order history rows
         (written every step, read for the features j >= 1); the observation; the reward; optional
-        host-fed demand and harness-metric rows; with a drawn-demand table (draw_layout), periods
-        t+1..t+3 written at t % 4 == 0 and read at the other periods.
+        host-fed demand and harness-metric rows. `handover=True` adds the drawn-demand table's bytes
+        (draw_layout: periods t+1..t+3 written at t % 4 == 0, read at the other periods): traffic of an
+        implementation choice, like the state record's unused slots, so not part of the algorithmic
+        figure the roofline is priced on (bench.py reports it beside it).
         """
         es, NP, _ = self.state_layout()
         s = self.spec
         N, T = s.num_nodes, s.num_periods
         d = [int(x) for x in s.delay]
         nbto, bto_es = self.split_layout()
-        dtab_es = 0 if host_demand else self.draw_layout()
+        dtab_es = self.draw_layout() if handover and not host_demand else 0
         split = nbto > 0
         hist = any(g in (nat.G_DEMAND_HIST, nat.G_ORDER_HIST) and j >= 1 for g, j in s.features)
         per = []

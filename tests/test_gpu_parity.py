@@ -362,14 +362,16 @@ def test_gpu_jit_and_aot_continue_each_others_episode(state_bytes, monkeypatch):
 def test_gpu_step_traffic_matches_bench_formula():
     """Algorithmic bytes per env-step for the bench layouts: C2 96 B steady,
     95.5 B averaged over the 30-period episode (t = 0 reads no state rows, node i no arrival
-    before t = d_i); with a drawn-demand table (imenv_draw_layout: small handles) + one byte per
-    retailer read at t % 4 != 0 and three written at t % 4 == 0 (periods t+1..t+3: 22 + 22 bytes over
-    the episode)."""
+    before t = d_i). The drawn-demand table (imenv_draw_layout: small handles) is counted only with
+    handover=True: + one byte per retailer read at t % 4 != 0 and three written at t % 4 == 0 (periods
+    t+1..t+3: 22 + 22 bytes over the episode)."""
     env = _env("MAIM", C2, 64)
     assert env.state_layout()[0] == 1
     dt = env.draw_layout()
     assert dt == (0 if os.environ.get("IMENV_DTAB") == "0" else 1)
     steady, avg = env.step_traffic()
+    assert steady == 96 and abs(avg - (96 - 15 / 30)) < 1e-9
+    steady, avg = env.step_traffic(handover=True)
     assert steady == 96 + dt and abs(avg - (96 + dt * 44 / 30 - 15 / 30)) < 1e-9
     env.close()
     env = _env("MAIM_div", C4, 64)     # td slot of node 1 (delay 2), backlog_to rows, no history rows
@@ -380,7 +382,8 @@ def test_gpu_step_traffic_matches_bench_formula():
     assert nb == 2 and be == (4 if os.environ.get("IMENV_BTO_BYTES") == "4" else 2)
     # two retailers: no drawn-demand table by default (imenv_draw_layout; capi dtab_es_for)
     assert env.draw_layout() == (1 if os.environ.get("IMENV_DTAB") == "1" else 0)
-    assert steady == 16 + 16 + 4 + 1 + 4 + 2 * nb * be + 96 + 8 + env.draw_layout() * env.spec.num_retailers
+    assert steady == 16 + 16 + 4 + 1 + 4 + 2 * nb * be + 96 + 8
+    assert env.step_traffic(handover=True)[0] == steady + env.draw_layout() * env.spec.num_retailers
     env.close()
 
 
