@@ -50,7 +50,9 @@ def test_gpu_drawn_demand_random_spec_matches_oracle(i, dtab, kernel, monkeypatc
     off = 37 * i
     env = tp._env(kind, cfg, n, env_offset=off)
     env.set_jit(1 if kernel == "jit" else 0)
-    ora = OracleEnv(kind, cfg, n_envs=n)
+    # the split's round-robin a phase at a time (pinned equal to the literal loops by
+    # tests/test_split_closed_form.py): capacities of ~40,000 take minutes per episode in the literal loops
+    ora = OracleEnv(kind, cfg, n_envs=n, split="closed")
     if dtab == "1":
         assert env.draw_layout() > 0
     else:

@@ -1,0 +1,20 @@
+# round-5 validation (after the drawn-demand hand-over): GPU suite, smoke, bench lines (driver form at 2^20, C5 shard default x3, C4, C3),
+# RCCL one-rank line with the graph gather, 2-rank rehearsal
+set -o pipefail
+O=${1:-gpurun_out/r5ad}; mkdir -p $O
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
+tail -2 $O/pytest_gpu.log
+[ $rc -le 1 ] || exit 1
+timeout -k 10 180 python __graft_entry__.py smoke > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err || exit 1
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || exit 1
+for i in 1 2 3; do
+  timeout -k 10 300 python bench.py --n-envs 131072 --no-cpu-baseline > $O/c5shard_$i.json 2> $O/c5shard_$i.err || exit 1
+done
+timeout -k 10 300 python bench.py --config C4 --no-cpu-baseline > $O/c4.json 2> $O/c4.err || exit 1
+timeout -k 10 300 python bench.py --config C3 --no-cpu-baseline > $O/c3.json 2> $O/c3.err || exit 1
+timeout -k 10 300 python bench.py --rccl-solo --n-envs 131072 --steps 60 --warmup 10 --no-cpu-baseline > $O/rccl_131072.json 2> $O/rccl_131072.err || exit 1
+timeout -k 10 300 python bench.py --gpus 2 --rehearse-one-gpu --steps 20 --warmup 5 --no-cpu-baseline > $O/rehearse2.json 2> $O/rehearse2.err || exit 1
+for f in $O/*.json; do python -c "
+import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); r=d['roofline']; print('$f', d['value'], d['ms_per_step'], r['kernel_us'], r['frac'], r['traffic'], r['launch_pacing'].get('launch'))"; done
+echo all done
