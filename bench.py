@@ -457,6 +457,11 @@ def main():
     if gather_on and not args.rehearse_one_gpu:
         # RCCL records start / end events around every collective on its own stream (Work._get_duration)
         os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")
+        # ... and takes those events from a cache: an event of an eager collective that the watchdog still
+        # polls could come back recorded in the capturing stream of the graph-captured gather pass, and
+        # the watchdog's query then aborts the process ("operation not permitted on an event last recorded
+        # in a capturing stream"): fresh events per collective
+        os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
     import torch
     import torch.distributed as dist
     from imenv import VectorInvEnv

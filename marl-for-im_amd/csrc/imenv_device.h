@@ -265,6 +265,17 @@ __device__ __forceinline__ uint4 philox4(uint32_t c0, uint32_t c1, uint32_t c2, 
   return make_uint4(c0, c1, c2, c3);
 }
 
+// The episode word through the constant address space: a scalar load even where the kernel also
+// stores through other pointers (the drawn-demand hand-over), which would otherwise make it a vector
+// load that queues behind the step's state loads. The word is written only by the reset kernel, an
+// earlier launch, so it is constant for the life of this one.
+__device__ __forceinline__ uint32_t load_episode_word(const uint32_t* p) {
+  return *(const __attribute__((address_space(4))) uint32_t*)(unsigned long long)p;
+}
+
+// (Round 5 tried a branch-free select on the index bits, which let the compiler issue the step's loads
+// before the draw: 1.5x slower per launch in normal runs at 2^20 and 131,072 envs, yet as fast as this
+// one under a rocprofv3 kernel trace, profiles/r05/ab/ab_word_select.log; not kept.)
 __device__ __forceinline__ uint32_t word_of(const uint4& b, int w) {
   return w == 0 ? b.x : (w == 1 ? b.y : (w == 2 ? b.z : b.w));
 }
@@ -1347,7 +1358,7 @@ __device__ __forceinline__ void step_finish(const P& p, const StepArgs& A, const
   const bool poisson = draw_here && p.demand_dist() == IMENV_DEMAND_POISSON;
   const bool need_ep = draw_here || (p.noisy_demand() && !cached) || (p.noisy_delay() && !p.has_delay_u());
   // (diagnostic IMENV_ABLATE & 32: no scalar load of the episode word)
-  const uint32_t ep = ((IMENV_ABLATE & 32) || !need_ep) ? 0u : *A.episode;
+  const uint32_t ep = ((IMENV_ABLATE & 32) || !need_ep) ? 0u : load_episode_word(A.episode);
   const uint32_t gid = A.env_offset + (uint32_t)e;
   const uint64_t seed = p.seed();
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
@@ -1851,6 +1862,17 @@ __device__ __forceinline__ void step_body(const P& p, const StepArgs& A, uint32_
   StepLoad<P> L[EPT];
 #pragma unroll
   for (int k = 0; k < EPT; ++k) step_load(p, A, eb + k * BS + tid, L[k]);
+#ifndef IMENV_LOAD_FENCE
+#define IMENV_LOAD_FENCE 1
+#endif
+  // Issue the loads here when the drawn-demand hand-over is on: the compiler otherwise places them after
+  // the t % 4 == 0 branch that draws four periods, behind the episode word's load and the draw (C2 at
+  // 131,072 envs: 3.89 -> 3.77 us per launch). Elsewhere the fence costs (C4 5.51 -> 5.83 us, C2 at 2^20
+  // 18.5 -> 19.1: profiles/r05/ab/ab_load_fence.log), so only hipRTC kernels with the table get it
+  // (IMENV_LOAD_FENCE=0: A/B through IMENV_JIT_OPTS)
+  if constexpr (IMENV_LOAD_FENCE && P::JIT) {
+    if (p.demand_layout() == IMENV_LAYOUT_DRAW && p.dtab_es() > 0) asm volatile("" ::: "memory");
+  }
   p.stage_tables(s_tab, poisson);
   constexpr int SSTR = stage_stride<P>();
   constexpr int SLAB = BS * SSTR * (P::OBS_STAGE64 ? 2 : 1);   // floats per BS-env slab
